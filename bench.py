@@ -1,0 +1,353 @@
+#!/usr/bin/env python3
+"""Bloom-filter build benchmark on MI355X (BASELINE.json metric: build keys/s + key-bytes GiB/s,
+device-resident, 1/2/4/8 GPUs).
+
+Default workload (N=1): BASELINE config 2 -- 100M x 16-byte keys, 10 bits/key
+(m = 1,000,000,000 bits, k = 10), keys already resident in HBM.  One step = BloomFilter::new's
+zeroed bit array (bf.rs:71) + build_filter_from_entries over the batch (bf.rs:126-128).
+With N > 1 (torchrun, one rank per GPU) every rank builds its own independent SSTable shard
+of the same size (config 4's compaction fan-in): weak scaling, no data-path collective.
+
+Also: --config 3 (100M variable-length Zipf keys + 50M negative probes), --config 5 (1B x 32 B,
+15 bits/key -> m saturates at u32::MAX, k = 4; keys split over ranks, OR all-reduce, full
+probe sweep), --e2e (keys in host memory: H2D + build + D2H through the C ABI's pipeline).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import velarixdb_amd as vbf  # noqa: E402
+from velarixdb_amd import workloads as wl  # noqa: E402
+from velarixdb_amd._lib import call  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def vp(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Ctx:
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=self.dev)
+        self.stream = torch.cuda.current_stream(self.dev)
+        self.sp = ctypes.c_void_p(self.stream.cuda_stream)
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def max_over_ranks(self, x):
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(self, x):
+        if self.world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def timed_steps(ctx, step, steps, warmup):
+    """W untimed steps, then K steps bracketed by barrier + synchronize; returns (wall_s, kernel_ms list)."""
+    for _ in range(warmup):
+        step(None)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    evs = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(evs)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ctx.barrier()
+    kms = [a.elapsed_time(b) for a, b in evs]
+    return ctx.max_over_ranks(t1 - t0), kms
+
+
+def cpu_baseline(keys_host, offsets_host, stride, n_sample, m, k, sample_desc, threads=1):
+    """The oracle (a port of bf.rs:126-128 -> :84-92) on this node's host cores."""
+    import oracle
+    from velarixdb_amd.keys import HostBatch
+    words = np.zeros((m + 31) // 32, np.uint32)
+    b = HostBatch(keys_host, offsets_host, stride, n_sample, 1)
+    t0 = time.perf_counter()
+    oracle.build_words(b, m, k, words=words, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n_sample / dt, "unit": "keys/s", "cores": threads, "kind": "port",
+            "sample": sample_desc, "seconds": round(dt, 3)}
+
+
+# ---------------------------------------------------------------------------------------
+def bench_fixed(ctx, args):
+    """Configs 2 / 4: fixed 16-byte keys, 10 bits per key, one filter per rank."""
+    n, L = args.keys, args.key_bytes
+    p = wl.fpr_for_bits_per_key(args.bits_per_key)
+    m, k = vbf.num_bits(n, p), vbf.num_hash_functions(vbf.num_bits(n, p), n)
+    seed = wl.SEED_CFG2 if ctx.world == 1 else wl.SEED_CFG4 + ctx.rank
+    keys = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
+    call("vbf_gen_fixed_dev", seed, 0, n, L, vp(keys), ctx.sp)
+    nwords = (m + 31) // 32
+    words = torch.empty(nwords, dtype=torch.int32, device=ctx.dev)
+
+    def step(evs):
+        words.zero_()  # BloomFilter::new: BitVec::from_elem(m, false) (bf.rs:71)
+        if evs is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(ctx.stream)
+        call("vbf_build_dev", vp(keys), None, L, n, 1, m, k, vp(words), ctx.sp)
+        if evs is not None:
+            b.record(ctx.stream)
+            evs.append((a, b))
+
+    wall, kms = timed_steps(ctx, step, args.steps, args.warmup)
+
+    # post-timing checks on the last build: every key present; fill ratio
+    cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
+    call("vbf_probe_count_dev", vp(keys), None, L, n, 1, m, k, vp(words), vp(cnt), ctx.sp)
+    pop = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
+    call("vbf_popcount_dev", vp(words), nwords, vp(pop), ctx.sp)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == n, "false negatives: %d of %d keys found" % (cnt.item(), n)
+
+    total_keys = ctx.sum_over_ranks(n) * args.steps
+    value = total_keys / wall
+    kavg = float(np.mean(kms)) / 1e3
+    bytes_per_key = L + m / (8.0 * n)
+    achieved = n * bytes_per_key / kavg / 1e9
+    res = {
+        "metric": "Bloom build keys/s (device-resident keys, bit-exact SipHash-1-3 filter)",
+        "value": value, "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "key_gib_per_s": value * L / 2**30,
+        "config": {"workload": "config%d: %dM x %dB keys per GPU, %d bits/key (m=%d, k=%d)%s" % (
+            2 if ctx.world == 1 else 4, n // 10**6, L, args.bits_per_key, m, k,
+            "" if ctx.world == 1 else ", one independent SSTable shard per GPU"),
+            "n_keys_per_gpu": n, "key_bytes": L, "m_bits": m, "k": k, "len_prefix": True,
+            "parallelism": "independent shards x%d" % ctx.world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_fixed<Build,16,len_prefix>", "kernel_ms": kavg * 1e3,
+                     "algorithmic_bytes_per_key": bytes_per_key,
+                     "siprounds_per_key": (L + 8) // 8 + 5 * k},
+        "fill_ratio": int(pop.item()) / m,
+    }
+    if ctx.world == 1 and ctx.rank == 0 and not args.no_cpu_baseline:
+        ns = args.cpu_sample
+        host = keys[: ns * L].cpu().numpy()
+        res["cpu_baseline"] = cpu_baseline(host, None, L, ns, m, k,
+                                           "first %d of the %d keys, same m=%d/k=%d, 1 thread, ref-faithful "
+                                           "(full SipHash per seed, u64 %%, serial like bf.rs:127)" % (ns, n, m, k))
+        if args.cpu_opt_threads:
+            t = args.cpu_opt_threads
+            res["cpu_opt"] = cpu_baseline(host, None, L, ns, m, k, "same sample, prefix-shared, %d threads" % t, threads=t)
+    return res
+
+
+def bench_var(ctx, args):
+    """Config 3: 100M variable-length (8..128 B Zipf) keys build + 50M negative probes."""
+    n = args.keys
+    p = wl.fpr_for_bits_per_key(args.bits_per_key)
+    m = vbf.num_bits(n, p)
+    k = vbf.num_hash_functions(m, n)
+    off_h = wl.var_offsets(wl.SEED_CFG3, 0, n)
+    off = torch.from_numpy(off_h.view(np.int64)).to(ctx.dev)
+    keys = torch.empty(int(off_h[-1]), dtype=torch.uint8, device=ctx.dev)
+    call("vbf_gen_var_dev", wl.SEED_CFG3, 0, n, vp(off), vp(keys), ctx.sp)
+    nn = args.neg_keys
+    noff_h = wl.var_offsets(wl.SEED_CFG3_NEG, 0, nn)
+    noff = torch.from_numpy(noff_h.view(np.int64)).to(ctx.dev)
+    nkeys = torch.empty(int(noff_h[-1]), dtype=torch.uint8, device=ctx.dev)
+    call("vbf_gen_var_dev", wl.SEED_CFG3_NEG, 0, nn, vp(noff), vp(nkeys), ctx.sp)
+    words = torch.empty((m + 31) // 32, dtype=torch.int32, device=ctx.dev)
+
+    def step(evs):
+        words.zero_()
+        if evs is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(ctx.stream)
+        call("vbf_build_dev", vp(keys), vp(off), 0, n, 1, m, k, vp(words), ctx.sp)
+        if evs is not None:
+            b.record(ctx.stream)
+            evs.append((a, b))
+
+    wall, kms = timed_steps(ctx, step, args.steps, args.warmup)
+    cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
+
+    def probe(evs):
+        cnt.zero_()
+        if evs is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(ctx.stream)
+        call("vbf_probe_count_dev", vp(nkeys), vp(noff), 0, nn, 1, m, k, vp(words), vp(cnt), ctx.sp)
+        if evs is not None:
+            b.record(ctx.stream)
+            evs.append((a, b))
+
+    pwall, pkms = timed_steps(ctx, probe, args.steps, 1)
+    fp = int(cnt.item())
+    mean_len = float(off_h[-1]) / n
+    value = ctx.sum_over_ranks(n) * args.steps / wall
+    kavg = float(np.mean(kms)) / 1e3
+    bpk = mean_len + 8 + m / (8.0 * n)
+    achieved = n * bpk / kavg / 1e9
+    return {
+        "metric": "Bloom build keys/s (device-resident variable-length keys)", "value": value,
+        "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "key_gib_per_s": value * mean_len / 2**30,
+        "config": {"workload": "config3: %dM var-length keys (Zipf 8..128 B, mean %.1f B), %d bits/key (m=%d, k=%d) + %dM negative probes"
+                   % (n // 10**6, mean_len, args.bits_per_key, m, k, nn // 10**6)},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_generic<Build,offsets>",
+                     "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_key": bpk},
+        "probe": {"keys_per_s": nn / (float(np.mean(pkms)) / 1e3), "false_positives": fp,
+                  "fpr": fp / nn, "kernel_ms": float(np.mean(pkms))},
+    }
+
+
+def bench_cfg5(ctx, args):
+    """Config 5: 1B x 32 B keys, 15 bits/key (m saturates at u32::MAX, k = 4), split over ranks;
+    partial filters OR-all-reduced; full positive probe sweep + negative FPR sample."""
+    from velarixdb_amd.dist import or_allreduce_, padded_words, shard_range
+    N, L = args.keys, 32
+    p = wl.fpr_for_bits_per_key(15)
+    m = vbf.num_bits(N, p)
+    k = vbf.num_hash_functions(m, N)
+    lo, hi = shard_range(N, ctx.rank, ctx.world)
+    n = hi - lo
+    keys = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
+    call("vbf_gen_fixed_dev", wl.SEED_CFG5, lo, n, L, vp(keys), ctx.sp)
+    nwords = (m + 31) // 32
+    buf, chunk = padded_words(nwords, ctx.world, ctx.dev)
+
+    def step(evs):
+        buf.zero_()
+        if evs is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(ctx.stream)
+        call("vbf_build_dev", vp(keys), None, L, n, 1, m, k, vp(buf), ctx.sp)
+        if evs is not None:
+            b.record(ctx.stream)
+            evs.append((a, b))
+        or_allreduce_(buf, chunk)
+
+    wall, kms = timed_steps(ctx, step, args.steps, args.warmup)
+    cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
+    t0 = time.perf_counter()
+    call("vbf_probe_count_dev", vp(keys), None, L, n, 1, m, k, vp(buf), vp(cnt), ctx.sp)
+    torch.cuda.synchronize()
+    sweep = ctx.max_over_ranks(time.perf_counter() - t0)
+    hits = int(ctx.sum_over_ranks(int(cnt.item())))
+    assert hits == N, "positive sweep found %d of %d" % (hits, N)
+    nn = args.neg_keys
+    nk = torch.empty(nn * L, dtype=torch.uint8, device=ctx.dev)
+    call("vbf_gen_fixed_dev", wl.SEED_CFG5 ^ 0xFF, N + ctx.rank * nn, nn, L, vp(nk), ctx.sp)
+    cnt.zero_()
+    call("vbf_probe_count_dev", vp(nk), None, L, nn, 1, m, k, vp(buf), vp(cnt), ctx.sp)
+    torch.cuda.synchronize()
+    fp = ctx.sum_over_ranks(int(cnt.item()))
+    value = N * args.steps / wall
+    return {
+        "metric": "Bloom build keys/s (1B-key single filter across GPUs)", "value": value,
+        "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u64", "data": "synthetic", "key_gib_per_s": value * L / 2**30,
+        "config": {"workload": "config5: %d x 32B keys, 15 bits/key -> m=%d (u32-saturated), k=%d; OR all-reduce over %d ranks" % (N, m, k, ctx.world)},
+        "build_kernel_ms": float(np.mean(kms)), "probe_sweep_keys_per_s": N / sweep,
+        "negatives": {"n": nn * ctx.world, "false_positives": fp, "fpr": fp / (nn * ctx.world)},
+    }
+
+
+def bench_e2e(ctx, args):
+    """Keys in host memory (memtable / compaction output): vbf_filter_set_host end to end."""
+    n, L = args.keys, 16
+    p = wl.fpr_for_bits_per_key(10)
+    keys = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
+    call("vbf_gen_fixed_dev", wl.SEED_CFG2, 0, n, L, vp(keys), ctx.sp)
+    host = keys.cpu().numpy()
+    del keys
+    from velarixdb_amd.keys import HostBatch
+    hb = HostBatch(host, None, L, n, 1)
+    times = []
+    for i in range(args.warmup + args.steps):
+        t0 = time.perf_counter()
+        bf = vbf.BloomFilter(p, n, device=ctx.local)
+        bf.set_batch(hb)
+        w = bf.words()  # D2H of the finished filter (written back with the SST)
+        t1 = time.perf_counter()
+        if i >= args.warmup:
+            times.append(t1 - t0)
+        del bf
+    t = float(np.median(times))
+    return {"metric": "Bloom build keys/s end-to-end (host keys: H2D + build + D2H)", "value": n / t,
+            "unit": "keys/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": t * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u64", "data": "synthetic", "config": {"workload": "config2 e2e %dM x 16B, filter %d words" % (n // 10**6, w.size)}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--keys", type=int, default=None)
+    ap.add_argument("--key-bytes", type=int, default=16)
+    ap.add_argument("--bits-per-key", type=int, default=10)
+    ap.add_argument("--neg-keys", type=int, default=None)
+    ap.add_argument("--e2e", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=2_000_000)
+    ap.add_argument("--cpu-opt-threads", type=int, default=16)
+    args = ap.parse_args()
+    ctx = Ctx(args)
+    if args.config == 5:
+        args.keys = args.keys or 1_000_000_000
+        args.neg_keys = args.neg_keys or 10_000_000
+        res = bench_cfg5(ctx, args)
+    elif args.config == 3:
+        args.keys = args.keys or 100_000_000
+        args.neg_keys = args.neg_keys or 50_000_000
+        res = bench_var(ctx, args)
+    elif args.e2e:
+        args.keys = args.keys or 100_000_000
+        res = bench_e2e(ctx, args)
+    else:
+        args.keys = args.keys or (100_000_000 if args.config == 2 else 50_000_000)
+        res = bench_fixed(ctx, args)
+    if ctx.rank == 0:
+        print(json.dumps(res), flush=True)
+    if ctx.world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

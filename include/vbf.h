@@ -1,0 +1,142 @@
+/*
+ * vbf.h -- C ABI of the MI355X (gfx950) Bloom-filter engine behind velarixdb's src/filter.
+ *
+ * This is the drop-in boundary.  Every entry point takes plain pointers and sizes, never
+ * aborts or throws across the ABI, and returns an int status (VBF_OK = 0) unless noted.
+ * The message of the last failure on the calling thread is available from vbf_last_error().
+ *
+ * Reference interface replaced (velarixdb 0.0.17, /root/reference):
+ *   BloomFilter struct                 src/filter/bf.rs:38-58      -> vbf_filter (opaque handle)
+ *   BloomFilter::new                   src/filter/bf.rs:62-81      -> vbf_filter_new / vbf_size
+ *   BloomFilter::set                   src/filter/bf.rs:84-92      -> vbf_filter_set_host / _dev
+ *   BloomFilter::contains              src/filter/bf.rs:95-105     -> vbf_filter_contains_host / _dev
+ *   BloomFilter::build_filter_from_entries src/filter/bf.rs:126-128 -> vbf_filter_set_host (batch)
+ *   BloomFilter::recover_meta          src/filter/bf.rs:135-150    -> vbf_filter_recover
+ *   BloomFilter::serialize             src/filter/bf.rs:158-172    -> vbf_filter_serialize
+ *   FilterFileNode::recover            src/fs/mod.rs:768-796       -> vbf_meta_parse
+ *   BloomFilter::clear                 src/filter/bf.rs:180-195    -> vbf_filter_clear
+ *   num_elements / num_bits / num_of_hash_functions bf.rs:198-213  -> vbf_filter_num_*
+ *   calculate_hash                     src/filter/bf.rs:222-227    -> vbf_hashes_dev (parity)
+ *   calculate_no_of_bits               src/filter/bf.rs:230-233    -> vbf_num_bits
+ *   calculate_no_of_hash_function      src/filter/bf.rs:236-239    -> vbf_num_hash_functions
+ *   Clone (shares the bit array)       src/filter/bf.rs:242-254    -> vbf_filter_clone
+ *   Default                            src/filter/bf.rs:256-267    -> vbf_filter_default
+ *
+ * Key batches.  `keys` holds the key bytes back to back.  When `offsets` is non-NULL it has
+ * n+1 nondecreasing entries and key j is keys[offsets[j] .. offsets[j+1]) (positions are
+ * absolute in `keys`; offsets[0] need not be 0); otherwise key j is
+ * keys[j*stride .. (j+1)*stride).  Offsets live where the keys live (device or host).  `len_prefix` = 1 hashes LE64(len) || key, which is
+ * Rust's `Hash for [u8]` / `Vec<u8>` (every production call site: memtable/mem.rs:209-210,224,
+ * key_range/range.rs:130,136,171, filter/bf.rs:127).  len_prefix = 0 hashes the bytes as given,
+ * for callers that pre-encode other Hash impls (usize -> 8 LE bytes, as bf.rs's tests use).
+ *
+ * Filter words.  ceil(m/32) uint32 words, bit i = words[i/32] bit (i%32): the storage of
+ * bit-vec 0.6.3 `BitVec<u32>` (Cargo.toml:19).  Builds OR into existing bits, never clear.
+ */
+#ifndef VBF_H
+#define VBF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VBF_OK 0
+#define VBF_EINVAL (-1)   /* bad argument (where the reference asserts: bf.rs:63-67)    */
+#define VBF_EHIP (-2)     /* HIP runtime / launch failure                               */
+#define VBF_ENOMEM (-3)   /* device or pinned-host allocation failed                    */
+#define VBF_ENODEV (-4)   /* no usable gfx950 device                                    */
+#define VBF_EDIVZERO (-5) /* m == 0 with k > 0: the reference panics (`% 0`, bf.rs:88)   */
+
+const char* vbf_version(void);
+const char* vbf_last_error(void); /* thread-local; "" when the last call succeeded */
+int vbf_device_count(int* count);
+
+/* ---- sizing (host arithmetic, glibc log, Rust `as u32` saturation) ---- */
+uint32_t vbf_num_bits(uint64_t n, double p);              /* bf.rs:230-233 */
+uint32_t vbf_num_hash_functions(uint32_t m, uint32_t n);  /* bf.rs:236-239 */
+/* bf.rs:62-70: asserts p >= 0 and n > 0 (-> VBF_EINVAL), m = num_bits(n, p),
+ * k = num_hash_functions(m, n as u32). */
+int vbf_size(double p, uint64_t n, uint32_t* m, uint32_t* k);
+
+/* ---- filter.db metadata: u32 k | u32 n | f64 p, little-endian, 16 bytes ---- */
+void vbf_meta_serialize(uint32_t k, uint32_t n, double p, uint8_t out[16]); /* bf.rs:158-172 */
+int vbf_meta_parse(const uint8_t* in, size_t len, uint32_t* k, uint32_t* n, double* p); /* fs/mod.rs:768-796 */
+
+/* ---- stateless kernels on device-resident buffers; `stream` is a hipStream_t (NULL = the
+ *      legacy default stream).  Calls are asynchronous on that stream. ---- */
+int vbf_build_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                  int len_prefix, uint32_t m, uint32_t k, uint32_t* words, void* stream);
+int vbf_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                  int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                  void* stream);
+/* Adds the number of keys the filter answers "present" for to *count_dev (device u64). */
+int vbf_probe_count_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                        int len_prefix, uint32_t m, uint32_t k, const uint32_t* words,
+                        unsigned long long* count_dev, void* stream);
+/* out[j*k + i] = calculate_hash(key_j, i) (bf.rs:222-227). */
+int vbf_hashes_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                   int len_prefix, uint32_t k, uint64_t* out, void* stream);
+/* dst |= src over nwords (16-byte aligned): merging partial filters of one key set. */
+int vbf_or_words_dev(uint32_t* dst, const uint32_t* src, uint64_t nwords, void* stream);
+/* *count_dev += popcount(words[0..nwords)). */
+int vbf_popcount_dev(const uint32_t* words, uint64_t nwords, unsigned long long* count_dev,
+                     void* stream);
+
+/* ---- synthetic key sets (benchmarks/tests; definitions in DESIGN.md, section Workloads) ---- */
+int vbf_gen_fixed_dev(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* out,
+                      void* stream);
+int vbf_gen_var_dev(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offsets,
+                    uint8_t* out, void* stream);
+
+/* ---- one-shot host-pointer variants: keys/words in host memory, chunked H2D through pinned
+ *      staging on `device`, synchronous.  Build ORs into `words` (nwords = ceil(m/32)). ---- */
+int vbf_build_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                   int len_prefix, uint32_t m, uint32_t k, uint32_t* words, uint64_t nwords,
+                   int device);
+int vbf_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                   int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint64_t nwords,
+                   uint8_t* out, int device);
+
+/* ---- BloomFilter handle: the bit array lives in HBM on `device` ---- */
+typedef struct vbf_filter vbf_filter;
+
+int vbf_filter_new(double p, uint64_t no_of_elements, int device, vbf_filter** out); /* bf.rs:62-81 */
+int vbf_filter_default(int device, vbf_filter** out);                               /* bf.rs:256-267 */
+/* recover_meta (bf.rs:135-150): k and n from the 16-byte metadata, m recomputed from n, bits 0. */
+int vbf_filter_recover(const uint8_t* meta, size_t len, int device, vbf_filter** out);
+int vbf_filter_clone(const vbf_filter* f, vbf_filter** out); /* shares the bit array, bf.rs:242-254 */
+void vbf_filter_free(vbf_filter* f);
+
+/* set over a batch (bf.rs:84-92 per key; build_filter_from_entries bf.rs:126-128).
+ * no_of_elements += n (u32, wrapping like AtomicU32::fetch_add). */
+int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets,
+                        uint64_t stride, uint64_t n, int len_prefix);
+int vbf_filter_set_dev(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                       uint64_t n, int len_prefix, void* stream);
+/* contains over a batch (bf.rs:95-105): out[j] = 1 when every one of the k bits is set. */
+int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uint64_t* offsets,
+                             uint64_t stride, uint64_t n, int len_prefix, uint8_t* out);
+int vbf_filter_contains_dev(const vbf_filter* f, const uint8_t* keys, const uint64_t* offsets,
+                            uint64_t stride, uint64_t n, int len_prefix, uint8_t* out, void* stream);
+
+uint32_t vbf_filter_num_bits(const vbf_filter* f);           /* bf.rs:204-207 */
+uint32_t vbf_filter_num_elements(const vbf_filter* f);       /* bf.rs:198-201 */
+uint32_t vbf_filter_num_hash_functions(const vbf_filter* f); /* bf.rs:210-213 */
+double vbf_filter_false_positive_rate(const vbf_filter* f);  /* bf.rs:54 */
+int vbf_filter_device(const vbf_filter* f);
+uint32_t* vbf_filter_words_dev(const vbf_filter* f); /* device pointer to the bit array */
+int vbf_filter_serialize(const vbf_filter* f, uint8_t out[16]); /* bf.rs:158-172 */
+/* clear (bf.rs:180-195): zero this filter's (shared) bits and return a fresh empty filter with
+ * the same m, k and p. */
+int vbf_filter_clear(vbf_filter* f, vbf_filter** out);
+/* Bit-array persistence: copy the ceil(m/32) words out / in. */
+int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords);
+int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nwords);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VBF_H */

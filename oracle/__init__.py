@@ -1,0 +1,129 @@
+"""CPU oracle for velarixdb's Bloom-filter path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this.  It is
+the checker, never the thing measured or shipped.  See oracle.c for the reference anchors
+(bf.rs file:line) and tests/golden/ for the vectors that pin it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "liboracle.so")
+
+
+def build():
+    src = os.path.join(HERE, "oracle.c")
+    if not os.path.exists(SO) or os.path.getmtime(SO) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return SO
+
+
+def _load():
+    if not os.path.exists(SO):
+        build()
+    L = ctypes.CDLL(SO)
+    vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    L.ora_siphash13.restype = u64
+    L.ora_siphash13.argtypes = [vp, ctypes.c_size_t]
+    L.ora_hash.restype = u64
+    L.ora_hash.argtypes = [vp, ctypes.c_size_t, i, u64]
+    L.ora_num_bits.restype = u32
+    L.ora_num_bits.argtypes = [u64, ctypes.c_double]
+    L.ora_num_hash.restype = u32
+    L.ora_num_hash.argtypes = [u32, u32]
+    L.ora_build.restype = i
+    L.ora_build.argtypes = [vp, vp, u64, u64, i, u32, u32, vp]
+    L.ora_build_mt.restype = i
+    L.ora_build_mt.argtypes = [vp, vp, u64, u64, i, u32, u32, vp, i]
+    L.ora_probe.restype = i
+    L.ora_probe.argtypes = [vp, vp, u64, u64, i, u32, u32, vp, vp]
+    L.ora_hashes.restype = None
+    L.ora_hashes.argtypes = [vp, vp, u64, u64, i, u32, vp]
+    L.ora_splitmix64.restype = u64
+    L.ora_splitmix64.argtypes = [u64]
+    L.ora_gen_fixed.restype = None
+    L.ora_gen_fixed.argtypes = [u64, u64, u64, u32, vp]
+    L.ora_gen_var_len.restype = u32
+    L.ora_gen_var_len.argtypes = [u64, u64]
+    L.ora_gen_var.restype = None
+    L.ora_gen_var.argtypes = [u64, u64, u64, vp, vp]
+    return L
+
+
+lib = _load()
+
+
+def siphash13(msg: bytes) -> int:
+    return lib.ora_siphash13(msg, len(msg))
+
+
+def calc_hash(key: bytes, seed: int, len_prefix: int = 1) -> int:
+    return lib.ora_hash(key, len(key), len_prefix, seed)
+
+
+def num_bits(n, p):
+    return int(lib.ora_num_bits(n, p))
+
+
+def num_hash(m, n):
+    return int(lib.ora_num_hash(m, n & 0xFFFFFFFF))
+
+
+def _ptrs(batch):
+    d = batch.data.ctypes.data if batch.data.size else None
+    o = batch.offsets.ctypes.data if batch.offsets is not None else None
+    return d, o
+
+
+def build_words(batch, m, k, words=None, threads=1):
+    """OR the batch into `words` (new zeroed array when None); returns the words."""
+    if words is None:
+        words = np.zeros((m + 31) // 32, dtype=np.uint32)
+    d, o = _ptrs(batch)
+    wp = words.ctypes.data if words.size else None
+    if threads > 1:
+        rc = lib.ora_build_mt(d, o, batch.stride, batch.n, batch.len_prefix, m, k, wp, threads)
+    else:
+        rc = lib.ora_build(d, o, batch.stride, batch.n, batch.len_prefix, m, k, wp)
+    if rc:
+        raise ZeroDivisionError("m == 0 with k > 0")
+    return words
+
+
+def probe(batch, m, k, words):
+    out = np.zeros(batch.n, dtype=np.uint8)
+    d, o = _ptrs(batch)
+    rc = lib.ora_probe(d, o, batch.stride, batch.n, batch.len_prefix, m, k,
+                       words.ctypes.data if words.size else None, out.ctypes.data if out.size else None)
+    if rc:
+        raise ZeroDivisionError("m == 0 with k > 0")
+    return out
+
+
+def hashes(batch, k):
+    out = np.zeros(batch.n * k, dtype=np.uint64)
+    d, o = _ptrs(batch)
+    lib.ora_hashes(d, o, batch.stride, batch.n, batch.len_prefix, k, out.ctypes.data if out.size else None)
+    return out.reshape(batch.n, k)
+
+
+def gen_fixed(seed, base, n, length):
+    out = np.zeros(n * length, dtype=np.uint8)
+    lib.ora_gen_fixed(seed, base, n, length, out.ctypes.data if out.size else None)
+    return out
+
+
+def gen_var_lengths(seed, base, n):
+    return np.array([lib.ora_gen_var_len(seed, base + j) for j in range(n)], dtype=np.uint64)
+
+
+def gen_var(seed, base, offsets):
+    """Bytes for keys base..base+n-1 laid out at offsets (offsets[0] == 0)."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offsets) - 1
+    out = np.zeros(int(offsets[-1]), dtype=np.uint8)
+    lib.ora_gen_var(seed, base, n, offsets.ctypes.data, out.ctypes.data if out.size else None)
+    return out

@@ -1,0 +1,303 @@
+/*
+ * oracle.c -- CPU restatement of velarixdb src/filter (TEST INFRASTRUCTURE ONLY; see oracle.h).
+ *
+ * Parity anchors (reference = /root/reference, velarixdb 0.0.17):
+ *   calculate_hash                bf.rs:222-227   -> ora_hash
+ *   calculate_no_of_bits          bf.rs:230-233   -> ora_num_bits
+ *   calculate_no_of_hash_function bf.rs:236-239   -> ora_num_hash
+ *   set / build_filter_from_entries bf.rs:84-92, :126-128 -> ora_build
+ *   contains                      bf.rs:95-105    -> ora_probe
+ * Third-party algorithms restated from their published definitions (not in the reference tree):
+ *   Rust std DefaultHasher = SipHash-1-3, keys (0,0) (Aumasson & Bernstein, "SipHash: a fast
+ *     short-input PRF", c=1 compression / d=3 finalization rounds as used by Rust std);
+ *     `Hash for [u8]` = write_usize(len) (8 bytes LE on x86-64) then write(bytes);
+ *     `write_u64(seed)` appends LE64(seed) to the same stream.
+ *   bit-vec 0.6.3 BitVec<u32>: set(i) = storage[i / 32] |= 1 << (i % 32).
+ * Pinned by tests/golden/ (Perl-header SipHash vectors + reference SST fixtures).
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ROTL(x, b) (uint64_t)(((x) << (b)) | ((x) >> (64 - (b))))
+#define SIPROUND                                                                                   \
+    do {                                                                                           \
+        v0 += v1; v1 = ROTL(v1, 13); v1 ^= v0; v0 = ROTL(v0, 32);                                 \
+        v2 += v3; v3 = ROTL(v3, 16); v3 ^= v2;                                                     \
+        v0 += v3; v3 = ROTL(v3, 21); v3 ^= v0;                                                     \
+        v2 += v1; v1 = ROTL(v1, 17); v1 ^= v2; v2 = ROTL(v2, 32);                                  \
+    } while (0)
+
+static uint64_t load_le64(const uint8_t* p) {
+    uint64_t v;
+    memcpy(&v, p, 8); /* x86-64 is little-endian */
+    return v;
+}
+
+/* Streaming SipHash-1-3 state, the shape of Rust's SipHasher13 (write / finish). */
+typedef struct {
+    uint64_t v0, v1, v2, v3;
+    uint64_t tail;   /* pending bytes, little-endian */
+    unsigned ntail;  /* 0..7 */
+    uint64_t length; /* total bytes written */
+} sip13;
+
+static void sip_init(sip13* s) {
+    s->v0 = 0x736f6d6570736575ULL; /* k0 = 0 */
+    s->v1 = 0x646f72616e646f6dULL; /* k1 = 0 */
+    s->v2 = 0x6c7967656e657261ULL;
+    s->v3 = 0x7465646279746573ULL;
+    s->tail = 0;
+    s->ntail = 0;
+    s->length = 0;
+}
+
+static void sip_compress(sip13* s, uint64_t m) {
+    uint64_t v0 = s->v0, v1 = s->v1, v2 = s->v2, v3 = s->v3;
+    v3 ^= m;
+    SIPROUND;
+    v0 ^= m;
+    s->v0 = v0; s->v1 = v1; s->v2 = v2; s->v3 = v3;
+}
+
+/* Byte-stream semantics; whole 8-byte words go straight to the compression function once
+ * the pending tail is empty (the same bulk path Rust's SipHasher13::write takes). */
+static void sip_write(sip13* s, const uint8_t* p, size_t len) {
+    s->length += len;
+    size_t i = 0;
+    while (i < len && s->ntail != 0) {
+        s->tail |= (uint64_t)p[i++] << (8 * s->ntail);
+        if (++s->ntail == 8) {
+            sip_compress(s, s->tail);
+            s->tail = 0;
+            s->ntail = 0;
+        }
+    }
+    for (; i + 8 <= len; i += 8) sip_compress(s, load_le64(p + i));
+    for (; i < len; ++i) s->tail |= (uint64_t)p[i] << (8 * s->ntail++);
+}
+
+static uint64_t sip_finish(const sip13* s) {
+    uint64_t v0 = s->v0, v1 = s->v1, v2 = s->v2, v3 = s->v3;
+    uint64_t b = ((s->length & 0xff) << 56) | s->tail;
+    v3 ^= b;
+    SIPROUND;
+    v0 ^= b;
+    v2 ^= 0xff;
+    SIPROUND;
+    SIPROUND;
+    SIPROUND;
+    return v0 ^ v1 ^ v2 ^ v3;
+}
+
+uint64_t ora_siphash13(const uint8_t* msg, size_t len) {
+    sip13 s;
+    sip_init(&s);
+    sip_write(&s, msg, len);
+    return sip_finish(&s);
+}
+
+static void write_u64(sip13* s, uint64_t v) {
+    uint8_t b[8];
+    for (int i = 0; i < 8; ++i) b[i] = (uint8_t)(v >> (8 * i));
+    sip_write(s, b, 8);
+}
+
+/* bf.rs:222-227: DefaultHasher::new(); key.hash(&mut h); h.write_u64(seed); h.finish() */
+uint64_t ora_hash(const uint8_t* key, size_t len, int len_prefix, uint64_t seed) {
+    sip13 s;
+    sip_init(&s);
+    if (len_prefix) write_u64(&s, (uint64_t)len); /* Hash for [u8]: write_length_prefix */
+    sip_write(&s, key, len);
+    write_u64(&s, seed);
+    return sip_finish(&s);
+}
+
+/* Rust `f64 as u32`: saturating, NaN -> 0, truncation toward zero. */
+static uint32_t f64_as_u32(double x) {
+    if (x != x) return 0;
+    if (x <= 0.0) return 0;
+    if (x >= 4294967295.0) return 4294967295u;
+    return (uint32_t)x;
+}
+
+/* bf.rs:230-233: -((n as f64 * p.ln()) / (2f64.ln()).powi(2)).ceil() as u32 */
+uint32_t ora_num_bits(uint64_t n, double p) {
+    const double ln2 = log(2.0);
+    double x = ((double)n * log(p)) / (ln2 * ln2);
+    return f64_as_u32(-ceil(x));
+}
+
+/* bf.rs:236-239: ((m as f64 / n as f64) * (2f64.ln()).ceil()) as u32 ; ln2.ceil() == 1.0 */
+uint32_t ora_num_hash(uint32_t m, uint32_t n) {
+    double x = ((double)m / (double)n) * ceil(log(2.0));
+    return f64_as_u32(x);
+}
+
+static inline const uint8_t* key_at(const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                                    uint64_t j, uint64_t* len) {
+    if (offsets) {
+        *len = offsets[j + 1] - offsets[j];
+        return keys + offsets[j];
+    }
+    *len = stride;
+    return keys + j * stride;
+}
+
+int ora_build(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+              int len_prefix, uint32_t m, uint32_t k, uint32_t* words) {
+    if (m == 0 && k > 0 && n > 0) return -1;
+    for (uint64_t j = 0; j < n; ++j) {           /* bf.rs:127 entries.iter().for_each(set) */
+        uint64_t len;
+        const uint8_t* key = key_at(keys, offsets, stride, j, &len);
+        for (uint32_t i = 0; i < k; ++i) {         /* bf.rs:86 */
+            uint64_t h = ora_hash(key, len, len_prefix, i);
+            uint64_t idx = h % (uint64_t)m;           /* bf.rs:88 */
+            words[idx >> 5] |= 1u << (idx & 31);     /* bf.rs:89, bit-vec LSB-first u32 */
+        }
+    }
+    return 0;
+}
+
+int ora_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+              int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out) {
+    if (m == 0 && k > 0 && n > 0) return -1;
+    for (uint64_t j = 0; j < n; ++j) {
+        uint64_t len;
+        const uint8_t* key = key_at(keys, offsets, stride, j, &len);
+        uint8_t hit = 1;                           /* bf.rs:104: vacuously true when k == 0 */
+        for (uint32_t i = 0; i < k; ++i) {
+            uint64_t idx = ora_hash(key, len, len_prefix, i) % (uint64_t)m;
+            if (!((words[idx >> 5] >> (idx & 31)) & 1u)) { hit = 0; break; } /* bf.rs:100-102 */
+        }
+        out[j] = hit;
+    }
+    return 0;
+}
+
+void ora_hashes(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                int len_prefix, uint32_t k, uint64_t* out) {
+    for (uint64_t j = 0; j < n; ++j) {
+        uint64_t len;
+        const uint8_t* key = key_at(keys, offsets, stride, j, &len);
+        for (uint32_t i = 0; i < k; ++i) out[j * k + i] = ora_hash(key, len, len_prefix, i);
+    }
+}
+
+/* ---- cpu-opt: prefix-shared hashing, threads OR private arrays together ---- */
+
+typedef struct {
+    const uint8_t* keys;
+    const uint64_t* offsets;
+    uint64_t stride, lo, hi;
+    int len_prefix;
+    uint32_t m, k;
+    uint32_t* words;
+} mt_job;
+
+static void* mt_worker(void* arg) {
+    mt_job* jb = (mt_job*)arg;
+    for (uint64_t j = jb->lo; j < jb->hi; ++j) {
+        uint64_t len;
+        const uint8_t* key = key_at(jb->keys, jb->offsets, jb->stride, j, &len);
+        sip13 pre;
+        sip_init(&pre);
+        if (jb->len_prefix) write_u64(&pre, len);
+        sip_write(&pre, key, len);
+        for (uint32_t i = 0; i < jb->k; ++i) {
+            sip13 s = pre;
+            write_u64(&s, i);
+            uint64_t idx = sip_finish(&s) % (uint64_t)jb->m;
+            jb->words[idx >> 5] |= 1u << (idx & 31);
+        }
+    }
+    return NULL;
+}
+
+int ora_build_mt(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                 int len_prefix, uint32_t m, uint32_t k, uint32_t* words, int threads) {
+    if (m == 0 && k > 0 && n > 0) return -1;
+    if (threads < 1) threads = 1;
+    uint64_t nwords = ((uint64_t)m + 31) / 32;
+    pthread_t* tid = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    mt_job* jobs = (mt_job*)calloc((size_t)threads, sizeof(mt_job));
+    for (int t = 0; t < threads; ++t) {
+        jobs[t] = (mt_job){keys, offsets, stride, n * t / threads, n * (t + 1) / threads,
+                           len_prefix, m, k, NULL};
+        jobs[t].words = t == 0 ? words : (uint32_t*)calloc(nwords ? nwords : 1, 4);
+        pthread_create(&tid[t], NULL, mt_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+    for (int t = 1; t < threads; ++t) {
+        for (uint64_t w = 0; w < nwords; ++w) words[w] |= jobs[t].words[w];
+        free(jobs[t].words);
+    }
+    free(jobs);
+    free(tid);
+    return 0;
+}
+
+/* ---- synthetic workloads ---- */
+
+uint64_t ora_splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+#define GOLDEN 0x9E3779B97F4A7C15ULL
+
+static uint64_t fixed_word(uint64_t seed, uint64_t j, uint64_t c) {
+    if (c == 0) return ora_splitmix64(seed ^ j);
+    if (c == 1) return j;
+    return ora_splitmix64(seed ^ j ^ (c * GOLDEN));
+}
+
+void ora_gen_fixed(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* out) {
+    for (uint64_t jj = 0; jj < n; ++jj) {
+        uint64_t j = base + jj;
+        uint8_t* o = out + jj * len;
+        for (uint32_t b = 0; b < len; ++b) o[b] = (uint8_t)(fixed_word(seed, j, b >> 3) >> (8 * (b & 7)));
+    }
+}
+
+/* Zipf(s = 1.1) on {1..121}: thresholds T[r] = floor(CDF(r) * 2^53), r = 1..120. */
+static uint64_t zipf_T[121];
+static int zipf_ready = 0;
+
+static void zipf_init(void) {
+    double w[122], total = 0.0;
+    for (int r = 1; r <= 121; ++r) { w[r] = pow((double)r, -1.1); total += w[r]; }
+    double acc = 0.0;
+    for (int r = 1; r <= 120; ++r) {
+        acc += w[r];
+        zipf_T[r] = (uint64_t)((acc / total) * 9007199254740992.0);
+    }
+    zipf_ready = 1;
+}
+
+uint32_t ora_gen_var_len(uint64_t seed, uint64_t j) {
+    if (!zipf_ready) zipf_init();
+    uint64_t u = ora_splitmix64(seed ^ j ^ 0xD1B54A32D192ED03ULL) >> 11;
+    uint32_t r = 1;
+    while (r <= 120 && u >= zipf_T[r]) ++r;
+    return 7 + r; /* 8..128 bytes */
+}
+
+/* Var key bytes: word 0 = (j << 8) | tag (tag = seed & 0xff), word c >= 1 = splitmix64(seed ^ j ^ c*GOLDEN). */
+void ora_gen_var(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offsets, uint8_t* out) {
+    for (uint64_t jj = 0; jj < n; ++jj) {
+        uint64_t j = base + jj;
+        uint64_t len = offsets[jj + 1] - offsets[jj];
+        uint8_t* o = out + offsets[jj];
+        for (uint64_t b = 0; b < len; ++b) {
+            uint64_t c = b >> 3;
+            uint64_t wv = c == 0 ? ((j << 8) | (seed & 0xff)) : ora_splitmix64(seed ^ j ^ (c * GOLDEN));
+            o[b] = (uint8_t)(wv >> (8 * (b & 7)));
+        }
+    }
+}

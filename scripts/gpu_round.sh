@@ -1,0 +1,35 @@
+#!/bin/bash
+# GPU-box session: smoke, parity tests, bench, rocprofv3 kernel-trace summary.
+# Every GPU step has its own time limit; the script stops at the first fault/abort/timeout.
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
+cd "$ROOT"
+OUT="$ROOT/gpurun_out"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STEPS="${STEPS:-smoke pytest bench prof}"
+
+run() {  # run NAME SECONDS CMD...
+    local name=$1 secs=$2; shift 2
+    echo "== $name: $*"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "rc=$rc"; tail -n 8 "$OUT/$name.log"
+    case $rc in
+        0|1) return 0 ;;   # pass, or ordinary test/assert failure: the GPU is fine
+        *) echo "STOP after $name (rc=$rc)"; exit $rc ;;
+    esac
+}
+
+for s in $STEPS; do
+  case $s in
+    smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) run pytest_gpu 1200 python -m pytest tests -x -q -m gpu ;;
+    bench)  run bench 600 python bench.py ;;
+    bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
+    bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;
+    e2e)    run bench_e2e 600 python bench.py --e2e --steps 3 --warmup 1 ;;
+    prof)   (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline) || exit $? ;;
+  esac
+done
+echo "ALL DONE"

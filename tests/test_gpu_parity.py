@@ -1,0 +1,331 @@
+"""Parity of the gfx950 path (through the C ABI) with the oracle and the golden vectors.
+
+Bar: bit-exact words, hashes and probe answers.  Small cases compare whole outputs with the
+oracle; the headline sizes (tests/test_gpu_scale.py) add size-independent properties.
+"""
+import ctypes
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from tests_util import parse_data_db, parse_filter_db
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _dev(arr):
+    t = torch.from_numpy(np.ascontiguousarray(arr)).to(DEV)
+    return t
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dev_batch(b):
+    """HostBatch -> (keys_t, offs_t) on the GPU."""
+    keys = _dev(b.data if b.data.size else np.zeros(1, np.uint8))
+    offs = _dev(b.offsets.view(np.int64)) if b.offsets is not None else None
+    return keys, offs
+
+
+def gpu_hashes(vbf, b, k):
+    keys, offs = dev_batch(b)
+    out = torch.zeros(max(b.n * k, 1), dtype=torch.int64, device=DEV)
+    vbf._lib.call("vbf_hashes_dev", _ptr(keys), _ptr(offs), b.stride, b.n, b.len_prefix, k,
+                  _ptr(out), _stream())
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint64)[: b.n * k].reshape(b.n, k)
+
+
+def gpu_build(vbf, b, m, k, words=None):
+    keys, offs = dev_batch(b)
+    nw = (m + 31) // 32
+    w = _dev(words.view(np.int32)) if words is not None else torch.zeros(max(nw, 1), dtype=torch.int32, device=DEV)
+    vbf._lib.call("vbf_build_dev", _ptr(keys), _ptr(offs), b.stride, b.n, b.len_prefix, m, k,
+                  _ptr(w), _stream())
+    torch.cuda.synchronize()
+    return w.cpu().numpy().view(np.uint32)[:nw]
+
+
+def gpu_probe(vbf, b, m, k, words):
+    keys, offs = dev_batch(b)
+    w = _dev(words.view(np.int32) if words.size else np.zeros(1, np.int32))
+    out = torch.zeros(max(b.n, 1), dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_probe_dev", _ptr(keys), _ptr(offs), b.stride, b.n, b.len_prefix, m, k,
+                  _ptr(w), _ptr(out), _stream())
+    cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    vbf._lib.call("vbf_probe_count_dev", _ptr(keys), _ptr(offs), b.stride, b.n, b.len_prefix, m, k,
+                  _ptr(w), _ptr(cnt), _stream())
+    torch.cuda.synchronize()
+    res = out.cpu().numpy()[: b.n]
+    assert int(cnt.item()) == int(res.sum())
+    return res
+
+
+# ----------------------------------------------------------------------------------------
+def test_hashes_match_golden(vbf, golden):
+    """calculate_hash (bf.rs:222-227) on the device == Perl-header SipHash vectors."""
+    from velarixdb_amd.keys import HostBatch
+    for v in golden("hashes"):
+        key = bytes.fromhex(v["key"])
+        arr = np.frombuffer(key, np.uint8).copy() if key else np.zeros(0, np.uint8)
+        b = HostBatch(arr, np.array([0, len(key)], np.uint64), 0, 1, v["len_prefix"])
+        h = gpu_hashes(vbf, b, len(v["h"]))
+        assert ["%016x" % x for x in h[0]] == v["h"], len(key)
+
+
+@pytest.mark.parametrize("L", [1, 5, 7, 8, 9, 15, 16, 17, 24, 31, 32, 33, 40, 64, 100])
+@pytest.mark.parametrize("lp", [1, 0])
+def test_hashes_fixed_stride_match_oracle(vbf, ora, L, lp):
+    from velarixdb_amd.keys import HostBatch
+    n, k = 3000, 7
+    data = ora.gen_fixed(0xABC + L, 0, n, L)
+    b = HostBatch(data, None, L, n, lp)
+    assert np.array_equal(gpu_hashes(vbf, b, k), ora.hashes(b, k))
+
+
+def test_hashes_variable_length_unaligned(vbf, ora):
+    """Offsets path with every start alignment, empty keys and a 65536-byte key (consts:7)."""
+    from velarixdb_amd.keys import pack
+    rng = np.random.default_rng(7)
+    keys = [bytes(rng.integers(0, 256, int(L), dtype=np.uint8)) for L in rng.integers(0, 70, 2000)]
+    keys += [b"", b"", bytes(range(256)) * 256]  # 65536 B
+    b = pack(keys)
+    assert np.array_equal(gpu_hashes(vbf, b, 5), ora.hashes(b, 5))
+    # shift the whole buffer by 1..7 bytes: same keys, every alignment
+    for shift in range(1, 8):
+        from velarixdb_amd.keys import HostBatch
+        data = np.concatenate([np.zeros(shift, np.uint8), b.data])
+        sb = HostBatch(data, b.offsets + np.uint64(shift), 0, b.n, 1)
+        assert np.array_equal(gpu_hashes(vbf, sb, 3), ora.hashes(b, 3))
+
+
+@pytest.mark.parametrize("L,lp,m,k", [(16, 1, 10_000_000, 10), (16, 1, 1, 3), (8, 0, 191701, 19),
+                                      (32, 1, 4_000_003, 4), (24, 1, 777_777, 7), (12, 1, 50_000, 5),
+                                      (16, 0, 65536, 33), (100, 1, 1_000_003, 2)])
+def test_build_fixed_matches_oracle(vbf, ora, L, lp, m, k):
+    from velarixdb_amd.keys import HostBatch
+    n = 200_000 if L <= 32 else 20_000
+    data = ora.gen_fixed(0x5EED0001, 0, n, L)
+    b = HostBatch(data, None, L, n, lp)
+    want = ora.build_words(b, m, k)
+    got = gpu_build(vbf, b, m, k)
+    assert np.array_equal(got, want)
+    # probe: every key present, plus disjoint negatives (j >= n) agree with the oracle
+    assert gpu_probe(vbf, b, m, k, got).all()
+    neg = HostBatch(ora.gen_fixed(0x5EED0002, n, 50_000, L), None, L, 50_000, lp)
+    assert np.array_equal(gpu_probe(vbf, neg, m, k, got), ora.probe(neg, m, k, want))
+
+
+def test_config1_bit_exact(vbf, ora):
+    """BASELINE config 1: 1M x 16 B, 10 bits/key -> m = 10,000,000, k = 10."""
+    from velarixdb_amd import num_bits, num_hash_functions
+    from velarixdb_amd.keys import HostBatch
+    from velarixdb_amd.workloads import SEED_CFG2, fpr_for_bits_per_key
+    n = 1_000_000
+    m = num_bits(n, fpr_for_bits_per_key(10))
+    k = num_hash_functions(m, n)
+    assert (m, k) == (10_000_000, 10)
+    b = HostBatch(ora.gen_fixed(SEED_CFG2, 0, n, 16), None, 16, n, 1)
+    want = ora.build_words(b, m, k, threads=8)
+    assert np.array_equal(gpu_build(vbf, b, m, k), want)
+
+
+def test_build_variable_length_matches_oracle(vbf, ora):
+    from velarixdb_amd.keys import pack_offsets
+    from velarixdb_amd.workloads import SEED_CFG3, SEED_CFG3_NEG, var_offsets
+    n, m, k = 100_000, 1_000_003, 10
+    off = var_offsets(SEED_CFG3, 0, n)
+    data = ora.gen_var(SEED_CFG3, 0, off)
+    b = pack_offsets(data, off)
+    want = ora.build_words(b, m, k)
+    got = gpu_build(vbf, b, m, k)
+    assert np.array_equal(got, want)
+    noff = var_offsets(SEED_CFG3_NEG, 0, 30_000)
+    nb = pack_offsets(ora.gen_var(SEED_CFG3_NEG, 0, noff), noff)
+    assert np.array_equal(gpu_probe(vbf, nb, m, k, got), ora.probe(nb, m, k, want))
+
+
+def test_device_generators_match_oracle(vbf, ora):
+    from velarixdb_amd.workloads import SEED_CFG3, var_offsets
+    for L in (16, 32, 13):
+        out = torch.zeros(1000 * L, dtype=torch.uint8, device=DEV)
+        vbf._lib.call("vbf_gen_fixed_dev", 0x5EED0001, 77, 1000, L, _ptr(out), _stream())
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ora.gen_fixed(0x5EED0001, 77, 1000, L))
+    off = var_offsets(SEED_CFG3, 500, 3000)
+    out = torch.zeros(int(off[-1]), dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_gen_var_dev", SEED_CFG3, 500, 3000, _ptr(_dev(off.view(np.int64))), _ptr(out), _stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ora.gen_var(SEED_CFG3, 500, off))
+
+
+def test_sst_fixture_rebuild_on_gpu(vbf, golden):
+    """range.rs:117-128 on the fixtures through the BloomFilter mirror (recover_meta + build)."""
+    want = {s["name"]: s for s in golden("sst_fixtures")["ssts"]}
+    root = os.path.join(GOLDEN, "sst_fixtures")
+    for name in sorted(os.listdir(root)):
+        bf = vbf.BloomFilter.default()
+        bf.file_path = os.path.join(root, name, "filter.db")
+        bf.recover_meta()
+        keys = parse_data_db(os.path.join(root, name, "data.db"))
+        k, n, p = parse_filter_db(bf.file_path)
+        assert (bf.no_of_hash_func, bf.no_of_elements, bf.false_positive_rate) == (k, n, p)
+        assert bf.num_bits() == want[name]["m"]
+        bf.build_filter_from_entries(keys)
+        assert bf.no_of_elements == n + len(keys)
+        w = bf.words()
+        assert hashlib.sha256(w.astype("<u4").tobytes()).hexdigest() == want[name]["sha256"]
+        assert bf.contains_many(keys).all()
+        assert int(bf.contains_many([b"zz%05d" % i for i in range(5000)]).sum()) == want[name]["neg_hits_zz5000"]
+        assert bf.contains(keys[0]) and bf.contains(b"head")
+
+
+def test_bf_rs_unit_tests_on_gpu(vbf, golden):
+    """bf.rs:275-424 restated against the device filter."""
+    from velarixdb_amd import BloomFilter, I32Vec
+    # test_set_and_contain (:275-291)
+    bf = BloomFilter(0.01, 10)
+    assert bf.num_elements() == 0 and bf.no_of_hash_func == 9 and bf.num_bits() == 95
+    bf.set(I32Vec((1, 2, 3, 4)))
+    assert bf.num_elements() == 1 and bf.contains(I32Vec((1, 2, 3, 4)))
+    # test_number_of_elements (:294-304)
+    bf = BloomFilter(0.01, 10)
+    for i in range(10):
+        bf.set(i)
+    assert bf.num_elements() == 10
+    # FPR tests (:307-424)
+    for v in golden("fpr_tests"):
+        p = float.fromhex(v["p"])
+        bf = BloomFilter(p, 10000)
+        bf.set_many(range(10000))
+        w = bf.words()
+        assert hashlib.sha256(w.astype("<u4").tobytes()).hexdigest() == v["sha256"]
+        fp = int(bf.contains_many(range(10000, 12000)).sum())
+        assert fp == v["false_positives"] and fp / 2000 <= p * 1.1
+
+
+def test_random_sets_on_gpu(vbf, golden):
+    from velarixdb_amd.keys import pack
+    for s in golden("random_sets"):
+        keys = [bytes.fromhex(x) for x in s["keys"]]
+        b = pack(keys)
+        if "words" in s:
+            got = gpu_build(vbf, b, s["m"], s["k"])
+            assert ["%08x" % x for x in got] == s["words"]
+            if "neg_keys" in s:
+                nb = pack([bytes.fromhex(x) for x in s["neg_keys"]])
+                assert gpu_probe(vbf, nb, s["m"], s["k"], got).tolist() == s["neg_hits"]
+        else:
+            h = gpu_hashes(vbf, b, s["k"])
+            assert (h % np.uint64(s["m"])).tolist() == s["indices"]
+
+
+def test_saturated_m_config5_shape(vbf, ora):
+    """m = u32::MAX (config 5 sizing): indices up to 2^32-2, 512 MiB words."""
+    from velarixdb_amd.keys import HostBatch
+    m, k, n = 4294967295, 4, 100_000
+    b = HostBatch(ora.gen_fixed(0x5EED0005, 0, n, 32), None, 32, n, 1)
+    got = gpu_build(vbf, b, m, k)
+    hs = ora.hashes(b, k) % np.uint64(m)
+    want = np.zeros((m + 31) // 32, np.uint32)
+    np.bitwise_or.at(want, (hs >> np.uint64(5)).astype(np.int64).ravel(),
+                     (np.uint32(1) << (hs & np.uint64(31)).astype(np.uint32)).ravel())
+    assert np.array_equal(got, want)
+
+
+def test_edge_cases(vbf, ora):
+    from velarixdb_amd import BloomFilter
+    from velarixdb_amd._lib import VBF_EDIVZERO, lib
+    from velarixdb_amd.keys import pack
+    # empty batch: no-op
+    w = gpu_build(vbf, pack([]), 1000, 5)
+    assert not w.any()
+    # k == 0 (p > 1): contains is vacuously true (bf.rs:104)
+    bf = BloomFilter(2.0, 5)
+    assert bf.num_bits() == 0 and bf.no_of_hash_func == 0
+    bf.set(b"a")
+    assert bf.contains(b"zzz")
+    # m == 0 with k > 0: the reference panics -> ZeroDivisionError / VBF_EDIVZERO
+    rc = lib.vbf_build_dev(None, None, 1, 1, 1, 0, 3, None, None)
+    assert rc == VBF_EDIVZERO
+    # duplicates are idempotent, OR accumulates into existing bits
+    b1 = pack([b"x", b"y"])
+    b2 = pack([b"x", b"x", b"y", b"y"])
+    assert np.array_equal(gpu_build(vbf, b1, 999, 4), gpu_build(vbf, b2, 999, 4))
+    base = np.zeros(32, np.uint32)
+    base[3] = 0xF0F0F0F0
+    got = gpu_build(vbf, b1, 1024, 4, words=base.copy())
+    assert np.array_equal(got, ora.build_words(b1, 1024, 4, words=base.copy()))
+
+
+def test_filter_handle_semantics(vbf, tmp_path):
+    from velarixdb_amd import BloomFilter
+    bf = BloomFilter(1e-4, 512)  # memtable sizing, mem.rs:188-191
+    assert (bf.num_bits(), bf.no_of_hash_func) == (9815, 19)
+    keys = [b"key%04d" % i for i in range(300)]
+    bf.set_many(keys)
+    c = bf.clone()  # shares bits (bf.rs:249)
+    c.set(b"extra")
+    assert bf.contains(b"extra")
+    assert bf.no_of_elements == 300 and c.no_of_elements == 301
+    # write / recover_meta (bf.rs:114-150): m recomputed from stored n
+    bf.write(tmp_path)
+    assert open(tmp_path / "filter.db", "rb").read() == bf.serialize()
+    r = BloomFilter.default()
+    r.file_path = str(tmp_path / "filter.db")
+    r.recover_meta()
+    assert r.no_of_hash_func == 19 and r.no_of_elements == 300
+    assert r.num_bits() == vbf.num_bits(300, 1e-4) and not r.words().any()
+    # clear (bf.rs:180-195): zeroes the shared array, fresh filter has same m, k, p
+    fresh = bf.clear()
+    assert not bf.words().any() and not c.words().any()
+    assert (fresh.num_bits(), fresh.no_of_hash_func, fresh.no_of_elements) == (9815, 19, 0)
+    # persistence of words round-trips
+    fresh.set_many(keys)
+    w = fresh.words()
+    other = BloomFilter(1e-4, 512)
+    other.load_words(w)
+    assert other.contains_many(keys).all()
+    # recover without a path
+    with pytest.raises(FileNotFoundError):
+        BloomFilter.default().recover_meta()
+
+
+def test_host_pointer_api_matches_device_api(vbf, ora):
+    """vbf_build_host / vbf_probe_host: chunked pinned-staging path == oracle (multi-chunk)."""
+    from velarixdb_amd._lib import call
+    from velarixdb_amd.workloads import SEED_CFG3, var_offsets
+    n, m, k = 3_000_000, 30_000_001, 7  # 48 MB of keys -> fixed path uses one chunk per 64 MB
+    data = ora.gen_fixed(0x77, 0, n, 16)
+    words = np.zeros((m + 31) // 32, np.uint32)
+    words[::97] = 0x1  # OR semantics with pre-set bits
+    want = words.copy()
+    call("vbf_build_host", data.ctypes.data, None, 16, n, 1, m, k, words.ctypes.data, words.size, 0)
+    from velarixdb_amd.keys import HostBatch
+    ora.build_words(HostBatch(data, None, 16, n, 1), m, k, words=want, threads=8)
+    assert np.array_equal(words, want)
+    out = np.zeros(n, np.uint8)
+    call("vbf_probe_host", data.ctypes.data, None, 16, n, 1, m, k, words.ctypes.data, words.size,
+         out.ctypes.data, 0)
+    assert out.all()
+    # variable length, > 64 MB of key bytes -> several chunks with rebased offsets
+    nv = 3_000_000
+    off = var_offsets(SEED_CFG3, 0, nv)
+    vdata = ora.gen_var(SEED_CFG3, 0, off)
+    assert off[-1] > 64 << 20
+    w2 = np.zeros((m + 31) // 32, np.uint32)
+    call("vbf_build_host", vdata.ctypes.data, off.ctypes.data, 0, nv, 1, m, k, w2.ctypes.data, w2.size, 0)
+    from velarixdb_amd.keys import pack_offsets
+    assert np.array_equal(w2, ora.build_words(pack_offsets(vdata, off), m, k, threads=8))

@@ -1,0 +1,12 @@
+"""velarixdb_amd -- MI355X-native Bloom-filter build/probe behind velarixdb's src/filter API.
+
+The compute path is libvbf.so (hand-written HIP for gfx950, C ABI in include/vbf.h); this
+package is its Python host mirror.  Importing it loads libvbf.so or raises -- there is no
+CPU fallback.
+"""
+from ._lib import LIB_PATH, VbfError, device_count, lib  # noqa: F401
+from .filter import (DEFAULT_FALSE_POSITIVE_RATE, FILTER_FILE_NAME, BloomFilter,  # noqa: F401
+                     num_bits, num_hash_functions)
+from .keys import HostBatch, I32Vec, RawMessage, Usize, pack, pack_fixed, pack_offsets  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,105 @@
+"""ctypes binding of the C ABI in include/vbf.h (libvbf.so, built in-tree for gfx950).
+
+There is no fallback: if the shared library is missing or fails to load, importing this
+module raises, so no product path can silently run on the CPU.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvbf.so")
+
+VBF_OK = 0
+VBF_EINVAL = -1
+VBF_EHIP = -2
+VBF_ENOMEM = -3
+VBF_ENODEV = -4
+VBF_EDIVZERO = -5
+
+_u8p = ctypes.c_void_p  # raw pointers (host or device) travel as integers
+_u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
+_int = ctypes.c_int
+_dbl = ctypes.c_double
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); must cover every function declared in include/vbf.h
+SIGNATURES = {
+    "vbf_version": (ctypes.c_char_p, []),
+    "vbf_last_error": (ctypes.c_char_p, []),
+    "vbf_device_count": (_int, [ctypes.POINTER(_int)]),
+    "vbf_num_bits": (_u32, [_u64, _dbl]),
+    "vbf_num_hash_functions": (_u32, [_u32, _u32]),
+    "vbf_size": (_int, [_dbl, _u64, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
+    "vbf_meta_serialize": (None, [_u32, _u32, _dbl, _vp]),
+    "vbf_meta_parse": (_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_u32), ctypes.POINTER(_u32),
+                              ctypes.POINTER(_dbl)]),
+    "vbf_build_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp]),
+    "vbf_probe_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _vp]),
+    "vbf_probe_count_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _vp]),
+    "vbf_hashes_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp]),
+    "vbf_or_words_dev": (_int, [_vp, _vp, _u64, _vp]),
+    "vbf_popcount_dev": (_int, [_vp, _u64, _vp, _vp]),
+    "vbf_gen_fixed_dev": (_int, [_u64, _u64, _u64, _u32, _vp, _vp]),
+    "vbf_gen_var_dev": (_int, [_u64, _u64, _u64, _vp, _vp, _vp]),
+    "vbf_build_host": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _u64, _int]),
+    "vbf_probe_host": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _u64, _vp, _int]),
+    "vbf_filter_new": (_int, [_dbl, _u64, _int, ctypes.POINTER(_vp)]),
+    "vbf_filter_default": (_int, [_int, ctypes.POINTER(_vp)]),
+    "vbf_filter_recover": (_int, [_vp, ctypes.c_size_t, _int, ctypes.POINTER(_vp)]),
+    "vbf_filter_clone": (_int, [_vp, ctypes.POINTER(_vp)]),
+    "vbf_filter_free": (None, [_vp]),
+    "vbf_filter_set_host": (_int, [_vp, _vp, _vp, _u64, _u64, _int]),
+    "vbf_filter_set_dev": (_int, [_vp, _vp, _vp, _u64, _u64, _int, _vp]),
+    "vbf_filter_contains_host": (_int, [_vp, _vp, _vp, _u64, _u64, _int, _vp]),
+    "vbf_filter_contains_dev": (_int, [_vp, _vp, _vp, _u64, _u64, _int, _vp, _vp]),
+    "vbf_filter_num_bits": (_u32, [_vp]),
+    "vbf_filter_num_elements": (_u32, [_vp]),
+    "vbf_filter_num_hash_functions": (_u32, [_vp]),
+    "vbf_filter_false_positive_rate": (_dbl, [_vp]),
+    "vbf_filter_device": (_int, [_vp]),
+    "vbf_filter_words_dev": (_vp, [_vp]),
+    "vbf_filter_serialize": (_int, [_vp, _vp]),
+    "vbf_filter_clear": (_int, [_vp, ctypes.POINTER(_vp)]),
+    "vbf_filter_words_to_host": (_int, [_vp, _vp, _u64]),
+    "vbf_filter_words_from_host": (_int, [_vp, _vp, _u64]),
+}
+
+
+class VbfError(RuntimeError):
+    """A nonzero status from the C ABI, carrying vbf_last_error()."""
+
+    def __init__(self, fn, code, msg):
+        super().__init__("%s failed (%d): %s" % (fn, code, msg))
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("velarixdb_amd: %s is missing; run __graft_entry__.build() "
+                          "(hipcc --offload-arch=gfx950). There is no CPU fallback." % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(fn_name, rc):
+    if rc != VBF_OK:
+        raise VbfError(fn_name, rc, lib.vbf_last_error().decode(errors="replace"))
+    return rc
+
+
+def call(fn_name, *args):
+    return check(fn_name, getattr(lib, fn_name)(*args))
+
+
+def device_count():
+    c = _int(0)
+    rc = lib.vbf_device_count(ctypes.byref(c))
+    return c.value if rc == VBF_OK else 0

@@ -1,0 +1,102 @@
+// sip13.hpp -- SipHash-1-3 (keys 0,0) for gfx950, split into a per-key prefix absorb and a
+// per-seed finish so that the k hashes of one key share the `LE64(len) || key` blocks.
+//
+// What is computed (velarixdb src/filter/bf.rs:222-227, Rust std DefaultHasher):
+//   h(key, i) = SipHash-1-3(k0=0, k1=0, [LE64(len(key))] || key || LE64(i))
+// The bracketed length block is present for byte keys (`Hash for [u8]`, every production call
+// site); callers that pre-encode integer keys pass len_prefix = 0.
+//
+// On the 32-bit VALU a 64-bit add is v_add_co/v_addc (2 ops), a rotate by 13/16/17/21 is two
+// v_alignbit_b32, and a rotate by 32 is a register rename, so one SipRound is ~24 VALU ops.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vbf {
+
+struct Sip {
+    uint64_t v0, v1, v2, v3;
+};
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+
+__device__ __forceinline__ void sip_round(Sip& s) {
+    s.v0 += s.v1; s.v1 = rotl64(s.v1, 13); s.v1 ^= s.v0; s.v0 = rotl64(s.v0, 32);
+    s.v2 += s.v3; s.v3 = rotl64(s.v3, 16); s.v3 ^= s.v2;
+    s.v0 += s.v3; s.v3 = rotl64(s.v3, 21); s.v3 ^= s.v0;
+    s.v2 += s.v1; s.v1 = rotl64(s.v1, 17); s.v1 ^= s.v2; s.v2 = rotl64(s.v2, 32);
+}
+
+__device__ __forceinline__ Sip sip_init() {
+    return Sip{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL,
+               0x7465646279746573ULL};
+}
+
+// c = 1 compression round per 8-byte block.
+__device__ __forceinline__ void sip_compress(Sip& s, uint64_t m) {
+    s.v3 ^= m;
+    sip_round(s);
+    s.v0 ^= m;
+}
+
+// Final block b (length byte << 56 | tail bytes) + d = 3 finalization rounds.
+__device__ __forceinline__ uint64_t sip_finish(Sip s, uint64_t b) {
+    s.v3 ^= b;
+    sip_round(s);
+    s.v0 ^= b;
+    s.v2 ^= 0xff;
+    sip_round(s);
+    sip_round(s);
+    sip_round(s);
+    return s.v0 ^ s.v1 ^ s.v2 ^ s.v3;
+}
+
+// State after absorbing every full block of the seed-independent prefix
+// P = [LE64(len)] || key (P bytes).  `tail` holds the last P % 8 bytes (r of them).
+struct Prefix {
+    Sip st;
+    uint64_t tail;
+    uint32_t r;      // P % 8
+    uint32_t total;  // (P + 8) & 0xff: the length byte of the final block
+};
+
+// Hash for seed i: one block (tail bytes || low bytes of LE64(i)), then the final block
+// (remaining seed bytes || length byte).  5 SipRounds per seed.
+__device__ __forceinline__ uint64_t prefix_hash(const Prefix& p, uint64_t seed) {
+    Sip s = p.st;
+    const uint32_t sb = p.r * 8;  // 0..56
+    // sb == 0: block = seed, tail = 0.  The double shift keeps every shift count < 64.
+    const uint64_t blk = p.tail | (seed << sb);
+    const uint64_t hi = (seed >> 1) >> (63 - sb);  // == seed >> (64 - sb), and 0 when sb == 0
+    sip_compress(s, blk);
+    return sip_finish(s, ((uint64_t)p.total << 56) | hi);
+}
+
+// Same, with P % 8 known at compile time (fixed-length keys).
+template <uint32_t R>
+__device__ __forceinline__ uint64_t prefix_hash_c(const Sip& st, uint64_t tail, uint32_t total,
+                                                  uint64_t seed) {
+    Sip s = st;
+    uint64_t blk, hi;
+    if constexpr (R == 0) {
+        blk = seed;
+        hi = 0;
+    } else {
+        blk = tail | (seed << (8 * R));
+        hi = seed >> (64 - 8 * R);
+    }
+    sip_compress(s, blk);
+    return sip_finish(s, ((uint64_t)total << 56) | hi);
+}
+
+// Exact x % m for 0 < m < 2^32 with mu = floor((2^64 - 1) / m) precomputed on the host.
+// q = mulhi(x, mu) is floor(x / m) or one less, so one conditional subtract finishes it
+// (bit-identical to Rust's `hash % bits.len() as u64`, bf.rs:88).
+__device__ __forceinline__ uint32_t fast_mod(uint64_t x, uint64_t m, uint64_t mu) {
+    const uint64_t q = __umul64hi(x, mu);
+    uint64_t r = x - q * m;
+    r = r >= m ? r - m : r;
+    return (uint32_t)r;
+}
+
+}  // namespace vbf

@@ -1,0 +1,677 @@
+// vbf_api.hip -- the C ABI (include/vbf.h) over the gfx950 kernels.
+//
+// Host-side responsibilities: argument checks that mirror the reference's asserts/panics,
+// sizing arithmetic (bf.rs:230-239), the filter handle (bf.rs:38-58 semantics: clones share
+// one bit array behind a mutex, like Arc<Mutex<BitVec>>), and the chunked, double-buffered
+// H2D pipeline for keys that arrive in host memory (memtable / compaction output).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/vbf.h"
+#include "vbf_kernels.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+inline int ok() {
+    g_err.clear();
+    return VBF_OK;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) {                                                               \
+            int code_ = (e_ == hipErrorOutOfMemory) ? VBF_ENOMEM : VBF_EHIP;                  \
+            return fail(code_, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+        }                                                                                     \
+    } while (0)
+
+// Switches the calling thread to `device` for the scope, restoring the previous one.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != device) err = hipSetDevice(device);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+#define DEVICE_SCOPE(dev)                                                                     \
+    DeviceGuard guard_(dev);                                                                  \
+    if (guard_.err != hipSuccess)                                                             \
+        return fail(VBF_ENODEV, "hipSetDevice(%d): %s", (int)(dev), hipGetErrorString(guard_.err))
+
+// Rust `f64 as u32`: saturating, NaN -> 0, truncation toward zero.
+uint32_t f64_as_u32(double x) {
+    if (std::isnan(x) || x <= 0.0) return 0;
+    if (x >= 4294967295.0) return 4294967295u;
+    return (uint32_t)x;
+}
+
+int check_keys(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n) {
+    if (n == 0) return VBF_OK;
+    if (!keys && !offsets && stride) return fail(VBF_EINVAL, "keys is NULL");
+    if (offsets == nullptr && stride == 0) return VBF_OK;  // n empty keys
+    return VBF_OK;
+}
+
+int check_mk(uint32_t m, uint32_t k, uint64_t n) {
+    if (m == 0 && k > 0 && n > 0)
+        return fail(VBF_EDIVZERO, "m == 0 with k = %u > 0: the reference divides by zero (bf.rs:88)", k);
+    return VBF_OK;
+}
+
+vbf::KeyBatch batch(const uint8_t* keys, const uint64_t* offsets, uint64_t off_base,
+                    uint64_t stride, uint64_t n, int lp) {
+    return vbf::KeyBatch{keys, offsets, off_base, stride, n, lp != 0};
+}
+
+// ---------------------------------------------------------------------------------------
+// Host -> device staging: two pinned buffers and two streams per device; chunk c uses
+// buffer (c & 1), so the H2D copy of chunk c+1 overlaps the kernel of chunk c.
+// ---------------------------------------------------------------------------------------
+constexpr uint64_t kChunkBytes = 64ull << 20;
+
+struct Staging {
+    std::mutex mu;
+    int device = -1;
+    hipStream_t stream[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    uint8_t* h_keys[2] = {nullptr, nullptr};
+    uint8_t* d_keys[2] = {nullptr, nullptr};
+    uint64_t key_cap[2] = {0, 0};
+    uint64_t* h_offs[2] = {nullptr, nullptr};
+    uint64_t* d_offs[2] = {nullptr, nullptr};
+    uint64_t off_cap[2] = {0, 0};
+    uint8_t* h_out[2] = {nullptr, nullptr};
+    uint8_t* d_out[2] = {nullptr, nullptr};
+    uint64_t out_cap[2] = {0, 0};
+    uint32_t* d_words = nullptr;  // scratch filter for the one-shot host API
+    uint64_t words_cap = 0;
+
+    int init(int dev) {
+        if (device == dev) return VBF_OK;
+        device = dev;
+        for (int b = 0; b < 2; ++b) {
+            HIP_TRY(hipStreamCreateWithFlags(&stream[b], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
+        }
+        return VBF_OK;
+    }
+    template <class T>
+    static int grow(T** h, T** d, uint64_t* cap, uint64_t count) {
+        if (count <= *cap) return VBF_OK;
+        if (h && *h) HIP_TRY(hipHostFree(*h));
+        if (*d) HIP_TRY(hipFree(*d));
+        if (h) *h = nullptr;
+        *d = nullptr;
+        *cap = 0;
+        uint64_t want = count + count / 4 + 64;
+        if (h) HIP_TRY(hipHostMalloc((void**)h, want * sizeof(T), hipHostMallocDefault));
+        HIP_TRY(hipMalloc((void**)d, want * sizeof(T)));
+        *cap = want;
+        return VBF_OK;
+    }
+};
+
+std::mutex g_staging_mu;
+std::vector<std::unique_ptr<Staging>> g_staging;
+
+Staging* staging_for(int device) {
+    std::lock_guard<std::mutex> lk(g_staging_mu);
+    if ((int)g_staging.size() <= device) g_staging.resize(device + 1);
+    if (!g_staging[device]) g_staging[device].reset(new Staging());
+    return g_staging[device].get();
+}
+
+// Streams host keys through the staging buffers, calling launch(batch_on_device, first_key,
+// buffer_index, stream) per chunk.  After the loop both streams are synchronized.
+template <class Launch, class AfterChunk>
+int pipeline_host_keys(Staging& st, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                       uint64_t n, int lp, bool need_out, Launch&& launch, AfterChunk&& after) {
+    uint64_t lo = 0;
+    int c = 0;
+    uint64_t pending_lo[2] = {0, 0}, pending_n[2] = {0, 0};
+    bool pending[2] = {false, false};
+    while (lo < n) {
+        // choose the chunk [lo, hi)
+        uint64_t hi, bytes, base = 0;
+        if (offsets) {
+            // largest hi with offsets[hi] - offsets[lo] <= kChunkBytes (a single huge key alone)
+            base = offsets[lo];
+            const uint64_t* ub = std::upper_bound(offsets + lo + 1, offsets + n + 1, base + kChunkBytes);
+            hi = (uint64_t)(ub - offsets) - 1;
+            if (hi <= lo) hi = lo + 1;
+            bytes = offsets[hi] - base;
+        } else {
+            uint64_t per = stride ? (kChunkBytes / stride) : n;
+            if (per == 0) per = 1;
+            hi = (n - lo) < per ? n : lo + per;
+            bytes = (hi - lo) * stride;
+        }
+        const int b = c & 1;
+        HIP_TRY(hipEventSynchronize(st.done[b]));  // buffer b free again
+        if (pending[b]) {
+            int rc = after(b, pending_lo[b], pending_n[b]);
+            if (rc) return rc;
+            pending[b] = false;
+        }
+        int rc = Staging::grow(&st.h_keys[b], &st.d_keys[b], &st.key_cap[b], bytes ? bytes : 1);
+        if (rc) return rc;
+        if (bytes) std::memcpy(st.h_keys[b], keys + (offsets ? base : lo * stride), bytes);
+        HIP_TRY(hipMemcpyAsync(st.d_keys[b], st.h_keys[b], bytes, hipMemcpyHostToDevice, st.stream[b]));
+        const uint64_t* d_off = nullptr;
+        if (offsets) {
+            rc = Staging::grow(&st.h_offs[b], &st.d_offs[b], &st.off_cap[b], hi - lo + 1);
+            if (rc) return rc;
+            std::memcpy(st.h_offs[b], offsets + lo, (hi - lo + 1) * sizeof(uint64_t));
+            HIP_TRY(hipMemcpyAsync(st.d_offs[b], st.h_offs[b], (hi - lo + 1) * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, st.stream[b]));
+            d_off = st.d_offs[b];
+        }
+        if (need_out) {
+            rc = Staging::grow(&st.h_out[b], &st.d_out[b], &st.out_cap[b], hi - lo);
+            if (rc) return rc;
+        }
+        vbf::KeyBatch kb = batch(st.d_keys[b], d_off, base, stride, hi - lo, lp);
+        rc = launch(kb, lo, b, st.stream[b]);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(st.done[b], st.stream[b]));
+        pending[b] = true;
+        pending_lo[b] = lo;
+        pending_n[b] = hi - lo;
+        lo = hi;
+        ++c;
+    }
+    for (int b = 0; b < 2; ++b) {
+        HIP_TRY(hipStreamSynchronize(st.stream[b]));
+        if (pending[b]) {
+            int rc = after(b, pending_lo[b], pending_n[b]);
+            if (rc) return rc;
+            pending[b] = false;
+        }
+    }
+    return VBF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Filter handle.  Storage is shared between clones (bf.rs:249 clones the Arc).
+// ---------------------------------------------------------------------------------------
+struct Storage {
+    int device = 0;
+    uint32_t m = 0;
+    uint64_t nwords = 0;
+    uint32_t* d_words = nullptr;
+    std::mutex mu;  // the reference's Mutex<BitVec>
+    ~Storage() {
+        if (d_words) {
+            int prev = -1;
+            (void)hipGetDevice(&prev);
+            (void)hipSetDevice(device);
+            (void)hipFree(d_words);
+            if (prev >= 0) (void)hipSetDevice(prev);
+        }
+    }
+};
+
+std::mutex g_stream_mu;
+std::vector<hipStream_t> g_filter_streams;
+
+int filter_stream(int device, hipStream_t* out) {
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    if ((int)g_filter_streams.size() <= device) g_filter_streams.resize(device + 1, nullptr);
+    if (!g_filter_streams[device]) HIP_TRY(hipStreamCreateWithFlags(&g_filter_streams[device], hipStreamNonBlocking));
+    *out = g_filter_streams[device];
+    return VBF_OK;
+}
+
+int new_storage(int device, uint32_t m, std::shared_ptr<Storage>* out) {
+    auto s = std::make_shared<Storage>();
+    s->device = device;
+    s->m = m;
+    s->nwords = ((uint64_t)m + 31) / 32;
+    if (s->nwords) {
+        hipStream_t st;
+        int rc = filter_stream(device, &st);
+        if (rc) return rc;
+        HIP_TRY(hipMalloc((void**)&s->d_words, s->nwords * 4));
+        HIP_TRY(hipMemsetAsync(s->d_words, 0, s->nwords * 4, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    *out = std::move(s);
+    return VBF_OK;
+}
+
+}  // namespace
+
+struct vbf_filter {
+    std::shared_ptr<Storage> bits;
+    uint32_t k = 0;
+    std::atomic<uint32_t> n{0};
+    double p = 0.0;
+};
+
+extern "C" {
+
+const char* vbf_version(void) { return "velarixdb_amd-vbf 0.1.0 gfx950"; }
+
+const char* vbf_last_error(void) { return g_err.c_str(); }
+
+int vbf_device_count(int* count) {
+    if (!count) return fail(VBF_EINVAL, "count is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(VBF_ENODEV, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = c;
+    return ok();
+}
+
+uint32_t vbf_num_bits(uint64_t n, double p) {
+    const double ln2 = std::log(2.0);
+    const double x = ((double)n * std::log(p)) / (ln2 * ln2);  // powi(2) == one multiply
+    return f64_as_u32(-std::ceil(x));
+}
+
+uint32_t vbf_num_hash_functions(uint32_t m, uint32_t n) {
+    const double x = ((double)m / (double)n) * std::ceil(std::log(2.0));  // ln2.ceil() == 1
+    return f64_as_u32(x);
+}
+
+int vbf_size(double p, uint64_t n, uint32_t* m, uint32_t* k) {
+    if (!m || !k) return fail(VBF_EINVAL, "NULL output");
+    if (!(p >= 0.0)) return fail(VBF_EINVAL, "False positive rate can not be less than or equal to zero");
+    if (n == 0) return fail(VBF_EINVAL, "No of elements should be greater than 0");
+    *m = vbf_num_bits(n, p);
+    *k = vbf_num_hash_functions(*m, (uint32_t)n);
+    return ok();
+}
+
+void vbf_meta_serialize(uint32_t k, uint32_t n, double p, uint8_t out[16]) {
+    uint64_t pb;
+    std::memcpy(&pb, &p, 8);
+    for (int i = 0; i < 4; ++i) out[i] = (uint8_t)(k >> (8 * i));
+    for (int i = 0; i < 4; ++i) out[4 + i] = (uint8_t)(n >> (8 * i));
+    for (int i = 0; i < 8; ++i) out[8 + i] = (uint8_t)(pb >> (8 * i));
+}
+
+int vbf_meta_parse(const uint8_t* in, size_t len, uint32_t* k, uint32_t* n, double* p) {
+    if (!in || !k || !n || !p) return fail(VBF_EINVAL, "NULL argument");
+    if (len < 16) return fail(VBF_EINVAL, "filter metadata truncated: %zu < 16 bytes (unexpected EOF)", len);
+    uint32_t kk = 0, nn = 0;
+    uint64_t pb = 0;
+    for (int i = 3; i >= 0; --i) kk = (kk << 8) | in[i];
+    for (int i = 3; i >= 0; --i) nn = (nn << 8) | in[4 + i];
+    for (int i = 7; i >= 0; --i) pb = (pb << 8) | in[8 + i];
+    *k = kk;
+    *n = nn;
+    std::memcpy(p, &pb, 8);
+    return ok();
+}
+
+// ---- stateless device-pointer entry points ----
+
+int vbf_build_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                  int len_prefix, uint32_t m, uint32_t k, uint32_t* words, void* stream) {
+    int rc = check_mk(m, k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    if (n && k && !words) return fail(VBF_EINVAL, "words is NULL");
+    vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+    HIP_TRY(vbf::launch_build(kb, m, k, words, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                  int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                  void* stream) {
+    int rc = check_mk(m, k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    if (n && !out) return fail(VBF_EINVAL, "out is NULL");
+    vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+    HIP_TRY(vbf::launch_probe(kb, m, k, words, out, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_probe_count_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                        int len_prefix, uint32_t m, uint32_t k, const uint32_t* words,
+                        unsigned long long* count_dev, void* stream) {
+    int rc = check_mk(m, k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    if (!count_dev) return fail(VBF_EINVAL, "count_dev is NULL");
+    vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+    HIP_TRY(vbf::launch_count(kb, m, k, words, count_dev, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_hashes_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                   int len_prefix, uint32_t k, uint64_t* out, void* stream) {
+    int rc = check_keys(keys, offsets, stride, n);
+    if (rc) return rc;
+    if (n && k && !out) return fail(VBF_EINVAL, "out is NULL");
+    vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+    HIP_TRY(vbf::launch_hashes(kb, k, out, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_or_words_dev(uint32_t* dst, const uint32_t* src, uint64_t nwords, void* stream) {
+    if (nwords && (!dst || !src)) return fail(VBF_EINVAL, "NULL words");
+    HIP_TRY(vbf::launch_or_words(dst, src, nwords, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_popcount_dev(const uint32_t* words, uint64_t nwords, unsigned long long* count_dev, void* stream) {
+    if (!count_dev || (nwords && !words)) return fail(VBF_EINVAL, "NULL argument");
+    HIP_TRY(vbf::launch_popcount(words, nwords, count_dev, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_gen_fixed_dev(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* out, void* stream) {
+    if (n && len && !out) return fail(VBF_EINVAL, "out is NULL");
+    HIP_TRY(vbf::launch_gen_fixed(seed, base, n, len, out, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_gen_var_dev(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offsets, uint8_t* out,
+                    void* stream) {
+    if (n && (!offsets || !out)) return fail(VBF_EINVAL, "NULL argument");
+    HIP_TRY(vbf::launch_gen_var(seed, base, n, offsets, out, (hipStream_t)stream));
+    return ok();
+}
+
+// ---- one-shot host-pointer entry points ----
+
+int vbf_build_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                   int len_prefix, uint32_t m, uint32_t k, uint32_t* words, uint64_t nwords,
+                   int device) {
+    int rc = check_mk(m, k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    const uint64_t need = ((uint64_t)m + 31) / 32;
+    if (nwords < need || (need && !words)) return fail(VBF_EINVAL, "words holds %llu < ceil(m/32) = %llu",
+                                                       (unsigned long long)nwords, (unsigned long long)need);
+    if (n == 0 || k == 0) return ok();
+    DEVICE_SCOPE(device);
+    Staging* st = staging_for(device);
+    std::lock_guard<std::mutex> lk(st->mu);
+    if ((rc = st->init(device))) return rc;
+    if ((rc = Staging::grow<uint32_t>(nullptr, &st->d_words, &st->words_cap, need))) return rc;
+    HIP_TRY(hipMemcpyAsync(st->d_words, words, need * 4, hipMemcpyHostToDevice, st->stream[0]));
+    HIP_TRY(hipEventRecord(st->done[0], st->stream[0]));
+    HIP_TRY(hipStreamWaitEvent(st->stream[1], st->done[0], 0));
+    rc = pipeline_host_keys(
+        *st, keys, offsets, stride, n, len_prefix, false,
+        [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t s) -> int {
+            HIP_TRY(vbf::launch_build(kb, m, k, st->d_words, s));
+            return VBF_OK;
+        },
+        [](int, uint64_t, uint64_t) { return VBF_OK; });
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(words, st->d_words, need * 4, hipMemcpyDeviceToHost));
+    return ok();
+}
+
+int vbf_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                   int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint64_t nwords,
+                   uint8_t* out, int device) {
+    int rc = check_mk(m, k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    const uint64_t need = ((uint64_t)m + 31) / 32;
+    if (nwords < need || (need && !words)) return fail(VBF_EINVAL, "words too short");
+    if (n && !out) return fail(VBF_EINVAL, "out is NULL");
+    if (n == 0) return ok();
+    DEVICE_SCOPE(device);
+    Staging* st = staging_for(device);
+    std::lock_guard<std::mutex> lk(st->mu);
+    if ((rc = st->init(device))) return rc;
+    if ((rc = Staging::grow<uint32_t>(nullptr, &st->d_words, &st->words_cap, need ? need : 1))) return rc;
+    if (need) HIP_TRY(hipMemcpyAsync(st->d_words, words, need * 4, hipMemcpyHostToDevice, st->stream[0]));
+    HIP_TRY(hipEventRecord(st->done[0], st->stream[0]));
+    HIP_TRY(hipStreamWaitEvent(st->stream[1], st->done[0], 0));
+    rc = pipeline_host_keys(
+        *st, keys, offsets, stride, n, len_prefix, true,
+        [&](const vbf::KeyBatch& kb, uint64_t, int b, hipStream_t s) -> int {
+            HIP_TRY(vbf::launch_probe(kb, m, k, st->d_words, st->d_out[b], s));
+            HIP_TRY(hipMemcpyAsync(st->h_out[b], st->d_out[b], kb.n, hipMemcpyDeviceToHost, s));
+            return VBF_OK;
+        },
+        [&](int b, uint64_t lo, uint64_t cnt) {
+            std::memcpy(out + lo, st->h_out[b], cnt);
+            return VBF_OK;
+        });
+    if (rc) return rc;
+    return ok();
+}
+
+// ---- filter handle ----
+
+static int make_filter(int device, uint32_t m, uint32_t k, double p, vbf_filter** out) {
+    if (!out) return fail(VBF_EINVAL, "out is NULL");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return fail(VBF_ENODEV, "no HIP device available");
+    if (device < 0 || device >= count) return fail(VBF_ENODEV, "device %d out of range (%d devices)", device, count);
+    DEVICE_SCOPE(device);
+    std::unique_ptr<vbf_filter> f(new vbf_filter());
+    int rc = new_storage(device, m, &f->bits);
+    if (rc) return rc;
+    f->k = k;
+    f->p = p;
+    *out = f.release();
+    return ok();
+}
+
+int vbf_filter_new(double p, uint64_t no_of_elements, int device, vbf_filter** out) {
+    uint32_t m, k;
+    int rc = vbf_size(p, no_of_elements, &m, &k);
+    if (rc) return rc;
+    return make_filter(device, m, k, p, out);
+}
+
+int vbf_filter_default(int device, vbf_filter** out) { return make_filter(device, 0, 0, 0.0, out); }
+
+int vbf_filter_recover(const uint8_t* meta, size_t len, int device, vbf_filter** out) {
+    uint32_t k, n;
+    double p;
+    int rc = vbf_meta_parse(meta, len, &k, &n, &p);
+    if (rc) return rc;
+    // bf.rs:144-147: m is recomputed from the STORED element count (usize) and p.
+    rc = make_filter(device, vbf_num_bits((uint64_t)n, p), k, p, out);
+    if (rc) return rc;
+    (*out)->n.store(n);
+    return ok();
+}
+
+int vbf_filter_clone(const vbf_filter* f, vbf_filter** out) {
+    if (!f || !out) return fail(VBF_EINVAL, "NULL argument");
+    vbf_filter* c = new vbf_filter();
+    c->bits = f->bits;
+    c->k = f->k;
+    c->n.store(f->n.load());
+    c->p = f->p;
+    *out = c;
+    return ok();
+}
+
+void vbf_filter_free(vbf_filter* f) { delete f; }
+
+uint32_t vbf_filter_num_bits(const vbf_filter* f) { return f ? f->bits->m : 0; }
+uint32_t vbf_filter_num_elements(const vbf_filter* f) { return f ? f->n.load() : 0; }
+uint32_t vbf_filter_num_hash_functions(const vbf_filter* f) { return f ? f->k : 0; }
+double vbf_filter_false_positive_rate(const vbf_filter* f) { return f ? f->p : 0.0; }
+int vbf_filter_device(const vbf_filter* f) { return f ? f->bits->device : -1; }
+uint32_t* vbf_filter_words_dev(const vbf_filter* f) { return f ? f->bits->d_words : nullptr; }
+
+int vbf_filter_serialize(const vbf_filter* f, uint8_t out[16]) {
+    if (!f || !out) return fail(VBF_EINVAL, "NULL argument");
+    vbf_meta_serialize(f->k, f->n.load(), f->p, out);
+    return ok();
+}
+
+int vbf_filter_set_dev(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                       uint64_t n, int len_prefix, void* stream) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    int rc = check_mk(s.m, f->k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    DEVICE_SCOPE(s.device);
+    {
+        std::lock_guard<std::mutex> lk(s.mu);
+        vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+        HIP_TRY(vbf::launch_build(kb, s.m, f->k, s.d_words, (hipStream_t)stream));
+    }
+    f->n.fetch_add((uint32_t)n);
+    return ok();
+}
+
+int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                        uint64_t n, int len_prefix) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    int rc = check_mk(s.m, f->k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    if (n && f->k) {
+        DEVICE_SCOPE(s.device);
+        Staging* st = staging_for(s.device);
+        std::lock_guard<std::mutex> lk(s.mu);
+        std::lock_guard<std::mutex> lk2(st->mu);
+        if ((rc = st->init(s.device))) return rc;
+        hipStream_t fs;
+        if ((rc = filter_stream(s.device, &fs))) return rc;
+        HIP_TRY(hipStreamSynchronize(fs));  // earlier async work on the filter stream
+        rc = pipeline_host_keys(
+            *st, keys, offsets, stride, n, len_prefix, false,
+            [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t hs) -> int {
+                HIP_TRY(vbf::launch_build(kb, s.m, f->k, s.d_words, hs));
+                return VBF_OK;
+            },
+            [](int, uint64_t, uint64_t) { return VBF_OK; });
+        if (rc) return rc;
+    }
+    f->n.fetch_add((uint32_t)n);
+    return ok();
+}
+
+int vbf_filter_contains_dev(const vbf_filter* f, const uint8_t* keys, const uint64_t* offsets,
+                            uint64_t stride, uint64_t n, int len_prefix, uint8_t* out, void* stream) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    int rc = check_mk(s.m, f->k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    if (n && !out) return fail(VBF_EINVAL, "out is NULL");
+    DEVICE_SCOPE(s.device);
+    std::lock_guard<std::mutex> lk(s.mu);
+    vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+    HIP_TRY(vbf::launch_probe(kb, s.m, f->k, s.d_words, out, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uint64_t* offsets,
+                             uint64_t stride, uint64_t n, int len_prefix, uint8_t* out) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    int rc = check_mk(s.m, f->k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    if (n && !out) return fail(VBF_EINVAL, "out is NULL");
+    if (n == 0) return ok();
+    DEVICE_SCOPE(s.device);
+    Staging* st = staging_for(s.device);
+    std::lock_guard<std::mutex> lk(s.mu);
+    std::lock_guard<std::mutex> lk2(st->mu);
+    if ((rc = st->init(s.device))) return rc;
+    hipStream_t fs;
+    if ((rc = filter_stream(s.device, &fs))) return rc;
+    HIP_TRY(hipStreamSynchronize(fs));
+    rc = pipeline_host_keys(
+        *st, keys, offsets, stride, n, len_prefix, true,
+        [&](const vbf::KeyBatch& kb, uint64_t, int b, hipStream_t hs) -> int {
+            HIP_TRY(vbf::launch_probe(kb, s.m, f->k, s.d_words, st->d_out[b], hs));
+            HIP_TRY(hipMemcpyAsync(st->h_out[b], st->d_out[b], kb.n, hipMemcpyDeviceToHost, hs));
+            return VBF_OK;
+        },
+        [&](int b, uint64_t lo, uint64_t cnt) {
+            std::memcpy(out + lo, st->h_out[b], cnt);
+            return VBF_OK;
+        });
+    if (rc) return rc;
+    return ok();
+}
+
+int vbf_filter_clear(vbf_filter* f, vbf_filter** out) {
+    if (!f || !out) return fail(VBF_EINVAL, "NULL argument");
+    Storage& s = *f->bits;
+    {
+        DEVICE_SCOPE(s.device);
+        std::lock_guard<std::mutex> lk(s.mu);
+        hipStream_t fs;
+        int rc = filter_stream(s.device, &fs);
+        if (rc) return rc;
+        if (s.nwords) HIP_TRY(hipMemsetAsync(s.d_words, 0, s.nwords * 4, fs));
+        HIP_TRY(hipStreamSynchronize(fs));
+    }
+    return make_filter(s.device, s.m, f->k, f->p, out);
+}
+
+int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    if (nwords < s.nwords || (s.nwords && !out)) return fail(VBF_EINVAL, "out holds %llu < %llu words",
+                                                            (unsigned long long)nwords, (unsigned long long)s.nwords);
+    if (!s.nwords) return ok();
+    DEVICE_SCOPE(s.device);
+    std::lock_guard<std::mutex> lk(s.mu);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, s.d_words, s.nwords * 4, hipMemcpyDeviceToHost));
+    return ok();
+}
+
+int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nwords) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    if (nwords != s.nwords || (s.nwords && !in)) return fail(VBF_EINVAL, "expected %llu words, got %llu",
+                                                            (unsigned long long)s.nwords, (unsigned long long)nwords);
+    if (!s.nwords) return ok();
+    DEVICE_SCOPE(s.device);
+    std::lock_guard<std::mutex> lk(s.mu);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(s.d_words, in, s.nwords * 4, hipMemcpyHostToDevice));
+    return ok();
+}
+
+}  // extern "C"

@@ -1,0 +1,368 @@
+// vbf_kernels.hip -- gfx950 kernels for velarixdb's Bloom-filter path.
+//
+//   Build  : BloomFilter::set over a key batch (bf.rs:84-92 via build_filter_from_entries :126-128)
+//   Probe  : BloomFilter::contains per key (bf.rs:95-105), one answer byte per key
+//   Count  : Probe + per-wave ballot popcount, one 64-bit atomic per wave (FPR sweeps)
+//   Hashes : the raw calculate_hash values (bf.rs:222-227), for parity tests
+//
+// Layout in HBM: keys packed back to back, either fixed stride (key j at j*stride) or
+// offsets[N+1] (u64, key j = [offsets[j]-off_base, offsets[j+1]-off_base)).  Filter =
+// ceil(m/32) u32 words, bit i = word[i>>5] bit (i&31) (bit-vec 0.6.3 BitVec<u32>).
+//
+// One lane per key: the lane absorbs the shared `LE64(len) || key` blocks once, then runs
+// 5 SipRounds per seed.  Fixed 8/16/24/32-byte keys get a specialised kernel with
+// 16-byte coalesced loads (the 100M x 16 B headline workload).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sip13.hpp"
+#include "vbf_kernels.hpp"
+
+namespace vbf {
+
+enum class Op { Build, Probe, Count, Hashes };
+
+struct Args {
+    const uint8_t* keys;
+    const uint64_t* offsets;
+    uint64_t off_base;
+    uint64_t stride;
+    uint64_t n;
+    uint64_t m;
+    uint64_t mu;
+    uint32_t k;
+    uint32_t* words;         // Build
+    const uint32_t* rwords;  // Probe / Count
+    uint8_t* out;            // Probe
+    uint64_t* out64;         // Hashes
+    unsigned long long* count;  // Count
+};
+
+constexpr int kBlock = 256;
+
+// The per-key action, given a callable hash(i) for seeds i = 0..k-1.  Returns the probe answer.
+template <Op OP, class H>
+__device__ __forceinline__ bool act(const Args& a, uint64_t j, const H& hash) {
+    if constexpr (OP == Op::Build) {
+        for (uint32_t i = 0; i < a.k; ++i) {
+            const uint32_t idx = fast_mod(hash(i), a.m, a.mu);
+            atomicOr(a.words + (idx >> 5), 1u << (idx & 31));  // no-return global_atomic_or
+        }
+        return true;
+    } else if constexpr (OP == Op::Hashes) {
+        for (uint32_t i = 0; i < a.k; ++i) a.out64[j * a.k + i] = hash(i);
+        return true;
+    } else {
+        bool hit = true;  // k == 0 -> vacuously true (bf.rs:104)
+        for (uint32_t i = 0; i < a.k; ++i) {
+            const uint32_t idx = fast_mod(hash(i), a.m, a.mu);
+            if (!((a.rwords[idx >> 5] >> (idx & 31)) & 1u)) {  // bf.rs:100-102 early exit
+                hit = false;
+                break;
+            }
+        }
+        if constexpr (OP == Op::Probe) a.out[j] = hit ? 1 : 0;
+        return hit;
+    }
+}
+
+template <Op OP>
+__device__ __forceinline__ void finish_count(const Args& a, bool hit) {
+    if constexpr (OP == Op::Count) {
+        const unsigned long long mask = __ballot(hit);
+        if ((threadIdx.x & 63) == 0 && mask) atomicAdd(a.count, (unsigned long long)__popcll(mask));
+    }
+}
+
+// ---- fixed-length keys, L % 8 == 0, compile-time L ----
+template <Op OP, uint32_t L, bool LP>
+__global__ __launch_bounds__(kBlock) void k_fixed(Args a) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool hit = false;
+    if (j < a.n) {
+        constexpr uint32_t NW = L / 8;
+        uint64_t w[NW];
+        const uint8_t* kp = a.keys + j * L;
+        if constexpr (NW % 2 == 0) {
+#pragma unroll
+            for (uint32_t c = 0; c < NW; c += 2) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(kp + 8 * c);
+                w[c] = v.x;
+                w[c + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t c = 0; c < NW; ++c) w[c] = *reinterpret_cast<const uint64_t*>(kp + 8 * c);
+        }
+        Sip st = sip_init();
+        if constexpr (LP) sip_compress(st, (uint64_t)L);
+#pragma unroll
+        for (uint32_t c = 0; c < NW; ++c) sip_compress(st, w[c]);
+        constexpr uint32_t total = (L + (LP ? 8 : 0) + 8) & 0xff;
+        hit = act<OP>(a, j, [&](uint32_t i) { return prefix_hash_c<0>(st, 0, total, i); });
+    }
+    finish_count<OP>(a, hit);
+}
+
+// Aligned 8-byte load of the word holding key bytes from `wbase + 8*i`, or 0 when that word
+// starts at or past `end` (never touches a word without a valid byte: no page can fault).
+__device__ __forceinline__ uint64_t ld_word(const uint64_t* wbase, uintptr_t wstart, uintptr_t end,
+                                            uint64_t i) {
+    return (wstart + 8 * i < end) ? wbase[i] : 0ull;
+}
+
+// Funnel: the 8 bytes starting `sh` bits into lo (sh in {0,8,...,56}).
+__device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh) {
+    return (lo >> sh) | ((hi << 1) << (63 - sh));
+}
+
+// ---- generic keys: runtime stride or offsets, any length (0 .. MAX_KEY_SIZE and beyond) ----
+template <Op OP, bool OFFS, bool LP>
+__global__ __launch_bounds__(kBlock) void k_generic(Args a) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool hit = false;
+    if (j < a.n) {
+        uint64_t beg, len;
+        if constexpr (OFFS) {
+            beg = a.offsets[j] - a.off_base;
+            len = a.offsets[j + 1] - a.offsets[j];
+        } else {
+            beg = j * a.stride;
+            len = a.stride;
+        }
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(a.keys + beg);
+        const uintptr_t end = addr + len;
+        const uintptr_t wstart = addr & ~(uintptr_t)7;
+        const uint64_t* wbase = reinterpret_cast<const uint64_t*>(wstart);
+        const uint32_t sh = (uint32_t)(addr & 7) * 8;
+
+        Sip st = sip_init();
+        if constexpr (LP) sip_compress(st, len);
+        const uint64_t nfull = len >> 3;
+        uint64_t lo = len ? ld_word(wbase, wstart, end, 0) : 0ull;
+        for (uint64_t c = 0; c < nfull; ++c) {
+            const uint64_t hi = ld_word(wbase, wstart, end, c + 1);
+            sip_compress(st, funnel(lo, hi, sh));
+            lo = hi;
+        }
+        Prefix p;
+        p.st = st;
+        p.r = (uint32_t)(len & 7);  // P % 8 == len % 8 (the length block is 8 bytes)
+        const uint64_t tmask = p.r ? (~0ull >> (64 - 8 * p.r)) : 0ull;
+        p.tail = p.r ? (funnel(lo, ld_word(wbase, wstart, end, nfull + 1), sh) & tmask) : 0ull;
+        p.total = (uint32_t)((len + (LP ? 8 : 0) + 8) & 0xff);
+        hit = act<OP>(a, j, [&](uint32_t i) { return prefix_hash(p, i); });
+    }
+    finish_count<OP>(a, hit);
+}
+
+// ---- host-side dispatch ----
+
+template <Op OP, uint32_t L, bool LP>
+static void launch_fixed(const Args& a, hipStream_t s) {
+    const uint64_t blocks = (a.n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((k_fixed<OP, L, LP>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+}
+
+template <Op OP, bool OFFS, bool LP>
+static void launch_generic(const Args& a, hipStream_t s) {
+    const uint64_t blocks = (a.n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL((k_generic<OP, OFFS, LP>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+}
+
+template <Op OP, bool LP>
+static void dispatch_lp(const Args& a, hipStream_t s) {
+    const bool aligned16 = (reinterpret_cast<uintptr_t>(a.keys) & 15) == 0;
+    const bool aligned8 = (reinterpret_cast<uintptr_t>(a.keys) & 7) == 0;
+    if (!a.offsets) {
+        if (a.stride == 16 && aligned16) return launch_fixed<OP, 16, LP>(a, s);
+        if (a.stride == 32 && aligned16) return launch_fixed<OP, 32, LP>(a, s);
+        if (a.stride == 8 && aligned8) return launch_fixed<OP, 8, LP>(a, s);
+        if (a.stride == 24 && aligned8) return launch_fixed<OP, 24, LP>(a, s);
+        return launch_generic<OP, false, LP>(a, s);
+    }
+    return launch_generic<OP, true, LP>(a, s);
+}
+
+template <Op OP>
+static void dispatch(const Args& a, bool lp, hipStream_t s) {
+    if (lp)
+        dispatch_lp<OP, true>(a, s);
+    else
+        dispatch_lp<OP, false>(a, s);
+}
+
+static Args make_args(const KeyBatch& kb, uint64_t m, uint32_t k) {
+    Args a{};
+    a.keys = kb.keys;
+    a.offsets = kb.offsets;
+    a.off_base = kb.off_base;
+    a.stride = kb.stride;
+    a.n = kb.n;
+    a.m = m;
+    a.mu = m ? (~0ull / m) : 0;
+    a.k = k;
+    return a;
+}
+
+// Largest grid one launch takes; bigger batches are split (keys never move).
+static constexpr uint64_t kMaxKeysPerLaunch = (uint64_t)kBlock * 0x7fffffffull;
+
+template <Op OP, class F>
+static hipError_t for_chunks(const KeyBatch& kb, F&& f) {
+    for (uint64_t lo = 0; lo < kb.n; lo += kMaxKeysPerLaunch) {
+        KeyBatch c = kb;
+        c.n = (kb.n - lo) < kMaxKeysPerLaunch ? (kb.n - lo) : kMaxKeysPerLaunch;
+        if (kb.offsets) {
+            c.offsets = kb.offsets + lo;
+        } else {
+            c.keys = kb.keys + lo * kb.stride;
+        }
+        f(c, lo);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_build(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, hipStream_t s) {
+    if (kb.n == 0 || k == 0) return hipSuccess;
+    return for_chunks<Op::Build>(kb, [&](const KeyBatch& c, uint64_t) {
+        Args a = make_args(c, m, k);
+        a.words = words;
+        dispatch<Op::Build>(a, c.len_prefix, s);
+    });
+}
+
+hipError_t launch_probe(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
+                        uint8_t* out, hipStream_t s) {
+    if (kb.n == 0) return hipSuccess;
+    return for_chunks<Op::Probe>(kb, [&](const KeyBatch& c, uint64_t lo) {
+        Args a = make_args(c, m, k);
+        a.rwords = words;
+        a.out = out + lo;
+        dispatch<Op::Probe>(a, c.len_prefix, s);
+    });
+}
+
+hipError_t launch_count(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
+                        unsigned long long* count, hipStream_t s) {
+    if (kb.n == 0) return hipSuccess;
+    return for_chunks<Op::Count>(kb, [&](const KeyBatch& c, uint64_t) {
+        Args a = make_args(c, m, k);
+        a.rwords = words;
+        a.count = count;
+        dispatch<Op::Count>(a, c.len_prefix, s);
+    });
+}
+
+hipError_t launch_hashes(const KeyBatch& kb, uint32_t k, uint64_t* out, hipStream_t s) {
+    if (kb.n == 0 || k == 0) return hipSuccess;
+    return for_chunks<Op::Hashes>(kb, [&](const KeyBatch& c, uint64_t lo) {
+        Args a = make_args(c, 0, k);
+        a.out64 = out + lo * k;
+        dispatch<Op::Hashes>(a, c.len_prefix, s);
+    });
+}
+
+// ---- bitwise OR of filter arrays (multi-GPU partial filters, bf.rs OR semantics) ----
+__global__ __launch_bounds__(kBlock) void k_or_words(uint32_t* dst, const uint32_t* src, uint64_t nw) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock * 4;
+    for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4; i < nw; i += stride) {
+        if (i + 4 <= nw) {
+            uint4 d = *reinterpret_cast<const uint4*>(dst + i);
+            const uint4 v = *reinterpret_cast<const uint4*>(src + i);
+            d.x |= v.x; d.y |= v.y; d.z |= v.z; d.w |= v.w;
+            *reinterpret_cast<uint4*>(dst + i) = d;
+        } else {
+            for (uint64_t t = i; t < nw; ++t) dst[t] |= src[t];
+        }
+    }
+}
+
+hipError_t launch_or_words(uint32_t* dst, const uint32_t* src, uint64_t nwords, hipStream_t s) {
+    if (nwords == 0) return hipSuccess;
+    uint64_t blocks = (nwords / 4 + kBlock - 1) / kBlock;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    const bool al = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
+    if (!al) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_or_words, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, nwords);
+    return hipGetLastError();
+}
+
+// ---- popcount of a filter (fill ratio reporting) ----
+__global__ __launch_bounds__(kBlock) void k_popcount(const uint32_t* w, uint64_t nw,
+                                                      unsigned long long* out) {
+    unsigned long long acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nw; i += stride)
+        acc += __popc(w[i]);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
+hipError_t launch_popcount(const uint32_t* words, uint64_t nwords, unsigned long long* out,
+                           hipStream_t s) {
+    if (nwords == 0) return hipSuccess;
+    uint64_t blocks = (nwords + kBlock - 1) / kBlock;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_popcount, dim3((unsigned)blocks), dim3(kBlock), 0, s, words, nwords, out);
+    return hipGetLastError();
+}
+
+// ---- synthetic workloads (bench / tests; same definitions as oracle/oracle.c) ----
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ULL;
+
+__global__ __launch_bounds__(kBlock) void k_gen_fixed(uint64_t seed, uint64_t base, uint64_t n,
+                                                       uint32_t len, uint8_t* out) {
+    const uint64_t jj = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (jj >= n) return;
+    const uint64_t j = base + jj;
+    uint8_t* o = out + jj * len;
+    if (len == 16 && ((reinterpret_cast<uintptr_t>(o) & 15) == 0)) {
+        *reinterpret_cast<ulonglong2*>(o) = ulonglong2{splitmix64(seed ^ j), j};
+        return;
+    }
+    for (uint32_t c = 0; c * 8 < len; ++c) {
+        const uint64_t w = c == 0 ? splitmix64(seed ^ j) : c == 1 ? j : splitmix64(seed ^ j ^ (c * kGolden));
+        for (uint32_t b = 0; b < 8 && c * 8 + b < len; ++b) o[c * 8 + b] = (uint8_t)(w >> (8 * b));
+    }
+}
+
+hipError_t launch_gen_fixed(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* out,
+                            hipStream_t s) {
+    if (n == 0 || len == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_fixed, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                       seed, base, n, len, out);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void k_gen_var(uint64_t seed, uint64_t base, uint64_t n,
+                                                     const uint64_t* offsets, uint8_t* out) {
+    const uint64_t jj = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (jj >= n) return;
+    const uint64_t j = base + jj;
+    const uint64_t beg = offsets[jj];
+    const uint64_t len = offsets[jj + 1] - offsets[jj];
+    uint8_t* o = out + beg;
+    for (uint64_t c = 0; c * 8 < len; ++c) {
+        const uint64_t w = c == 0 ? ((j << 8) | (seed & 0xff)) : splitmix64(seed ^ j ^ (c * kGolden));
+        for (uint32_t b = 0; b < 8 && c * 8 + b < len; ++b) o[c * 8 + b] = (uint8_t)(w >> (8 * b));
+    }
+}
+
+hipError_t launch_gen_var(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offsets,
+                          uint8_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_var, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                       seed, base, n, offsets, out);
+    return hipGetLastError();
+}
+
+}  // namespace vbf

@@ -1,0 +1,34 @@
+// vbf_kernels.hpp -- internal launch interface between the C ABI (vbf_api.hip) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vbf {
+
+// A batch of keys resident in device memory.
+//   offsets == nullptr : key j = keys[j*stride .. j*stride + stride)
+//   offsets != nullptr : key j = keys[offsets[j]-off_base .. offsets[j+1]-off_base)
+struct KeyBatch {
+    const uint8_t* keys;
+    const uint64_t* offsets;
+    uint64_t off_base;
+    uint64_t stride;
+    uint64_t n;
+    bool len_prefix;  // prepend LE64(len) (Rust `Hash for [u8]`)
+};
+
+hipError_t launch_build(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, hipStream_t s);
+hipError_t launch_probe(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
+                        uint8_t* out, hipStream_t s);
+hipError_t launch_count(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
+                        unsigned long long* count, hipStream_t s);
+hipError_t launch_hashes(const KeyBatch& kb, uint32_t k, uint64_t* out, hipStream_t s);
+hipError_t launch_or_words(uint32_t* dst, const uint32_t* src, uint64_t nwords, hipStream_t s);
+hipError_t launch_popcount(const uint32_t* words, uint64_t nwords, unsigned long long* out,
+                           hipStream_t s);
+hipError_t launch_gen_fixed(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* out,
+                            hipStream_t s);
+hipError_t launch_gen_var(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offsets,
+                          uint8_t* out, hipStream_t s);
+
+}  // namespace vbf

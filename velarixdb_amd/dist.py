@@ -1,0 +1,55 @@
+"""Multi-GPU layout of the Bloom-filter path.  One process per GPU.
+
+* Independent SSTables (compaction fan-in, compactors/sized.rs:170-200): each rank builds its
+  own shard's filter.  No data-path collective -- weak scaling.
+* One filter over a key set split across ranks (BASELINE config 5): each rank ORs its keys
+  into a full-width partial array, then the partials are merged with a bitwise-OR
+  all-reduce.  RCCL has no OR reduction, so it is composed from data movement plus a local
+  OR: all_to_all_single (rank r receives every rank's copy of bit-range r: a reduce-scatter
+  by bit range), the OR of those copies (HIP kernel vbf_or_words_dev on the GPU), then
+  all_gather_into_tensor so every rank holds the full filter for its probe sweep.
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from ._lib import call
+
+
+def shard_range(n, rank, world):
+    """Contiguous [lo, hi) of n items for `rank`: sizes differ by at most one."""
+    lo = n * rank // world
+    hi = n * (rank + 1) // world
+    return lo, hi
+
+
+def _or_into(acc, src):
+    """acc |= src, same shape int32 tensors."""
+    if acc.device.type == "cuda":
+        stream = ctypes.c_void_p(torch.cuda.current_stream(acc.device).cuda_stream)
+        call("vbf_or_words_dev", ctypes.c_void_p(acc.data_ptr()), ctypes.c_void_p(src.data_ptr()),
+             acc.numel(), stream)
+    else:  # gloo (CPU) process groups: the world_size>1 tests of this exchange
+        acc.bitwise_or_(src)
+
+
+def padded_words(nwords, world, device):
+    """An int32 buffer for nwords words padded so each rank's bit range is 16-B aligned."""
+    chunk = -(-nwords // world)
+    chunk = (chunk + 3) // 4 * 4
+    return torch.zeros(chunk * world, dtype=torch.int32, device=device), chunk
+
+
+def or_allreduce_(buf, chunk, group=None):
+    """In place: buf (padded_words layout) becomes the OR of every rank's buf."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return buf
+    recv = torch.empty_like(buf)
+    dist.all_to_all_single(recv, buf, group=group)
+    acc = recv[:chunk].clone()
+    for r in range(1, world):
+        _or_into(acc, recv[r * chunk:(r + 1) * chunk])
+    dist.all_gather_into_tensor(buf, acc, group=group)
+    return buf

@@ -1,0 +1,239 @@
+"""BloomFilter -- velarixdb's src/filter API on the gfx950 engine (C ABI in include/vbf.h).
+
+Mirrors /root/reference/src/filter/bf.rs (velarixdb 0.0.17) method for method, with the bit
+array resident in HBM.  Argument checks raise where the reference asserts or panics:
+
+  BloomFilter::new(p, n)            bf.rs:62-81    -> BloomFilter(p, n)       AssertionError
+  set(key)                          bf.rs:84-92    -> set(key)                ZeroDivisionError
+  contains(key)                     bf.rs:95-105   -> contains(key)           (m == 0 and k > 0)
+  write(dir)                        bf.rs:114-123  -> write(dir)
+  build_filter_from_entries(e)      bf.rs:126-128  -> build_filter_from_entries(e)  (one batch)
+  recover_meta()                    bf.rs:135-150  -> recover_meta()
+  serialize()                       bf.rs:158-172  -> serialize()
+  set_sstable_path / clear          bf.rs:175-195
+  num_elements / num_bits / num_of_hash_functions / get_sst_dir  bf.rs:198-219
+  Clone (shares the bit array)      bf.rs:242-254  -> clone() / copy.copy()
+  Default                           bf.rs:256-267  -> BloomFilter.default()
+
+Batch forms (set_many / contains_many and the *_dev variants taking device pointers) are the
+accelerated entry points the compaction build (compactors/sized.rs:192-193), the lazy
+recovery rebuild (key_range/range.rs:117-128) and bulk probes use.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+from ._lib import VBF_EDIVZERO, VBF_EINVAL, VbfError, call, lib
+from .keys import HostBatch, encode, pack
+
+FILTER_FILE_NAME = "filter"  # consts/mod.rs:27
+DEFAULT_FALSE_POSITIVE_RATE = 1e-4  # consts/mod.rs:17
+
+
+def num_bits(n, p):
+    """calculate_no_of_bits (bf.rs:230-233)."""
+    return int(lib.vbf_num_bits(n, p))
+
+
+def num_hash_functions(m, n):
+    """calculate_no_of_hash_function (bf.rs:236-239); n is `as u32`."""
+    return int(lib.vbf_num_hash_functions(m, n & 0xFFFFFFFF))
+
+
+def _raise(fn, exc):
+    code = exc.code
+    if code == VBF_EDIVZERO:
+        raise ZeroDivisionError("attempt to calculate the remainder with a divisor of zero "
+                                "(bf.rs:88): %s" % exc) from None
+    if code == VBF_EINVAL:
+        raise AssertionError(str(exc)) from None
+    raise exc
+
+
+class BloomFilter:
+    """A Bloom filter whose bits live in MI355X HBM; see the module docstring."""
+
+    def __init__(self, false_positive_rate=None, no_of_elements=None, device=0, _handle=None):
+        self.sst_dir = None
+        self.file_path = None
+        if _handle is not None:
+            self._h = _handle
+            return
+        h = ctypes.c_void_p()
+        try:
+            call("vbf_filter_new", float(false_positive_rate), int(no_of_elements), device, ctypes.byref(h))
+        except VbfError as e:
+            _raise("new", e)
+        self._h = h
+
+    # -- constructors ------------------------------------------------------------------
+    @classmethod
+    def default(cls, device=0):
+        h = ctypes.c_void_p()
+        call("vbf_filter_default", device, ctypes.byref(h))
+        return cls(_handle=h)
+
+    def clone(self):
+        h = ctypes.c_void_p()
+        call("vbf_filter_clone", self._h, ctypes.byref(h))
+        c = BloomFilter(_handle=h)
+        c.sst_dir, c.file_path = self.sst_dir, self.file_path
+        return c
+
+    __copy__ = clone
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.vbf_filter_free(h)
+            self._h = None
+
+    # -- fields (bf.rs:38-58) ------------------------------------------------------------
+    @property
+    def no_of_hash_func(self):
+        return int(lib.vbf_filter_num_hash_functions(self._h))
+
+    @property
+    def no_of_elements(self):
+        return int(lib.vbf_filter_num_elements(self._h))
+
+    @property
+    def false_positive_rate(self):
+        return float(lib.vbf_filter_false_positive_rate(self._h))
+
+    @property
+    def device(self):
+        return int(lib.vbf_filter_device(self._h))
+
+    def num_elements(self):
+        return self.no_of_elements
+
+    def num_bits(self):
+        return int(lib.vbf_filter_num_bits(self._h))
+
+    def num_of_hash_functions(self):
+        return self.no_of_hash_func
+
+    def num_words(self):
+        return (self.num_bits() + 31) // 32
+
+    def words_dev_ptr(self):
+        return lib.vbf_filter_words_dev(self._h)
+
+    def get_sst_dir(self):
+        if self.sst_dir is None:
+            raise ValueError("called `Option::unwrap()` on a `None` value (bf.rs:218)")
+        return self.sst_dir
+
+    def set_sstable_path(self, path):
+        self.sst_dir = os.fspath(path)
+
+    # -- set / contains ----------------------------------------------------------------
+    def set(self, key):
+        """bf.rs:84-92 for one key (a batch of one on the GPU)."""
+        self.set_many([key])
+
+    def contains(self, key):
+        """bf.rs:95-105 for one key."""
+        return bool(self.contains_many([key])[0])
+
+    def set_batch(self, b: HostBatch):
+        d, o = b.ptrs()
+        try:
+            call("vbf_filter_set_host", self._h, d, o, b.stride, b.n, b.len_prefix)
+        except VbfError as e:
+            _raise("set", e)
+
+    def contains_batch(self, b: HostBatch):
+        out = np.zeros(b.n, dtype=np.uint8)
+        d, o = b.ptrs()
+        try:
+            call("vbf_filter_contains_host", self._h, d, o, b.stride, b.n, b.len_prefix,
+                 out.ctypes.data if b.n else None)
+        except VbfError as e:
+            _raise("contains", e)
+        return out.astype(bool)
+
+    def set_many(self, keys):
+        self.set_batch(keys if isinstance(keys, HostBatch) else pack(keys))
+
+    def contains_many(self, keys):
+        return self.contains_batch(keys if isinstance(keys, HostBatch) else pack(keys))
+
+    def build_filter_from_entries(self, entries):
+        """bf.rs:126-128: `entries` is a sorted map (keys = Vec<u8>) or any iterable of keys."""
+        keys = entries.keys() if hasattr(entries, "keys") else entries
+        self.set_many(keys)
+
+    # device-resident batches (pointers from torch tensors or the C ABI)
+    def set_dev(self, keys_ptr, offsets_ptr, stride, n, len_prefix=1, stream=None):
+        try:
+            call("vbf_filter_set_dev", self._h, keys_ptr, offsets_ptr, stride, n, len_prefix, stream)
+        except VbfError as e:
+            _raise("set", e)
+
+    def contains_dev(self, keys_ptr, offsets_ptr, stride, n, out_ptr, len_prefix=1, stream=None):
+        try:
+            call("vbf_filter_contains_dev", self._h, keys_ptr, offsets_ptr, stride, n, len_prefix,
+                 out_ptr, stream)
+        except VbfError as e:
+            _raise("contains", e)
+
+    # -- bits ----------------------------------------------------------------------------
+    def words(self):
+        """The bit array as uint32 words (bit-vec BitVec<u32> storage)."""
+        w = np.zeros(self.num_words(), dtype=np.uint32)
+        call("vbf_filter_words_to_host", self._h, w.ctypes.data if w.size else None, w.size)
+        return w
+
+    def load_words(self, words):
+        w = np.ascontiguousarray(words, dtype=np.uint32)
+        call("vbf_filter_words_from_host", self._h, w.ctypes.data if w.size else None, w.size)
+
+    def clear(self):
+        """bf.rs:180-195: zero the shared bits, return a fresh empty filter (same m, k, p)."""
+        h = ctypes.c_void_p()
+        call("vbf_filter_clear", self._h, ctypes.byref(h))
+        return BloomFilter(_handle=h)
+
+    # -- metadata / files --------------------------------------------------------------
+    def serialize(self):
+        """bf.rs:158-172: u32 k | u32 n | f64 p, little-endian."""
+        buf = (ctypes.c_uint8 * 16)()
+        call("vbf_filter_serialize", self._h, buf)
+        return bytes(buf)
+
+    def write(self, dir_path):
+        """bf.rs:114-123: write `filter.db` (metadata only) and remember its path."""
+        path = os.path.join(os.fspath(dir_path), FILTER_FILE_NAME + ".db")
+        with open(path, "wb") as f:
+            f.write(self.serialize())
+        self.file_path = path
+
+    def recover_meta(self):
+        """bf.rs:135-150: k and n from filter.db, m recomputed from n, zeroed bits."""
+        if self.file_path is None:
+            raise FileNotFoundError("File path for filter not provided (err/mod.rs:19-20)")
+        try:
+            with open(self.file_path, "rb") as f:
+                meta = f.read(16)
+        except OSError:
+            raise FileNotFoundError("Error opening filter file %s" % self.file_path) from None
+        buf = (ctypes.c_uint8 * max(len(meta), 1)).from_buffer_copy(meta.ljust(max(len(meta), 1), b"\0"))
+        h = ctypes.c_void_p()
+        try:
+            call("vbf_filter_recover", buf, len(meta), self.device, ctypes.byref(h))
+        except VbfError as e:
+            if e.code == VBF_EINVAL:
+                raise EOFError("unexpected EOF reading %s" % self.file_path) from None
+            raise
+        old = self._h
+        self._h = h
+        lib.vbf_filter_free(old)
+
+    def __repr__(self):
+        return "BloomFilter(m=%d, k=%d, n=%d, p=%g, device=%d)" % (
+            self.num_bits(), self.no_of_hash_func, self.no_of_elements, self.false_positive_rate,
+            self.device)
