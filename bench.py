@@ -73,21 +73,33 @@ class Ctx:
 
 
 def timed_steps(ctx, step, steps, warmup):
-    """W untimed steps, then K steps bracketed by barrier + synchronize; returns (wall_s, kernel_ms list)."""
+    """W untimed steps, then K steps bracketed by barrier + synchronize.
+
+    Returns (max-over-ranks wall seconds, torch-event ms per step, library phase timings).
+    The library brackets each kernel phase with hipEvents on the launch stream."""
+    from velarixdb_amd._lib import lib, profile_read
     for _ in range(warmup):
         step(None)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
     evs = []
+    lib.vbf_profile_enable(1)
+    profile_read()  # reset
     t0 = time.perf_counter()
     for _ in range(steps):
         step(evs)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     ctx.barrier()
+    lib.vbf_profile_enable(0)
+    phases = profile_read()
     kms = [a.elapsed_time(b) for a, b in evs]
-    return ctx.max_over_ranks(t1 - t0), kms
+    return ctx.max_over_ranks(t1 - t0), kms, phases
+
+
+def phase_report(phases, steps):
+    return {p: {"ms_per_launch": ms / n, "launches": n} for p, (ms, n) in phases.items() if n}
 
 
 def cpu_baseline(keys_host, offsets_host, stride, n_sample, m, k, sample_desc, threads=1):
@@ -120,12 +132,12 @@ def bench_fixed(ctx, args):
         if evs is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(ctx.stream)
-        call("vbf_build_dev", vp(keys), None, L, n, 1, m, k, vp(words), ctx.sp)
+        call("vbf_build_dev_ex", vp(keys), None, L, n, 1, m, k, vp(words), args.strategy, ctx.sp)
         if evs is not None:
             b.record(ctx.stream)
             evs.append((a, b))
 
-    wall, kms = timed_steps(ctx, step, args.steps, args.warmup)
+    wall, kms, phases = timed_steps(ctx, step, args.steps, args.warmup)
 
     # post-timing checks on the last build: every key present; fill ratio
     cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
@@ -153,9 +165,10 @@ def bench_fixed(ctx, args):
             "parallelism": "independent shards x%d" % ctx.world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_fixed<Build,16,len_prefix>", "kernel_ms": kavg * 1e3,
+                     "kernel": "build (all phases of one vbf_build_dev_ex launch)", "kernel_ms": kavg * 1e3,
                      "algorithmic_bytes_per_key": bytes_per_key,
-                     "siprounds_per_key": (L + 8) // 8 + 5 * k},
+                     "siprounds_per_key": (L + 8) // 8 + 5 * k,
+                     "phases": phase_report(phases, args.steps)},
         "fill_ratio": int(pop.item()) / m,
     }
     if ctx.world == 1 and ctx.rank == 0 and not args.no_cpu_baseline:
@@ -192,12 +205,12 @@ def bench_var(ctx, args):
         if evs is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(ctx.stream)
-        call("vbf_build_dev", vp(keys), vp(off), 0, n, 1, m, k, vp(words), ctx.sp)
+        call("vbf_build_dev_ex", vp(keys), vp(off), 0, n, 1, m, k, vp(words), args.strategy, ctx.sp)
         if evs is not None:
             b.record(ctx.stream)
             evs.append((a, b))
 
-    wall, kms = timed_steps(ctx, step, args.steps, args.warmup)
+    wall, kms, phases = timed_steps(ctx, step, args.steps, args.warmup)
     cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
 
     def probe(evs):
@@ -210,7 +223,7 @@ def bench_var(ctx, args):
             b.record(ctx.stream)
             evs.append((a, b))
 
-    pwall, pkms = timed_steps(ctx, probe, args.steps, 1)
+    pwall, pkms, pphases = timed_steps(ctx, probe, args.steps, 1)
     fp = int(cnt.item())
     mean_len = float(off_h[-1]) / n
     value = ctx.sum_over_ranks(n) * args.steps / wall
@@ -253,13 +266,13 @@ def bench_cfg5(ctx, args):
         if evs is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(ctx.stream)
-        call("vbf_build_dev", vp(keys), None, L, n, 1, m, k, vp(buf), ctx.sp)
+        call("vbf_build_dev_ex", vp(keys), None, L, n, 1, m, k, vp(buf), args.strategy, ctx.sp)
         if evs is not None:
             b.record(ctx.stream)
             evs.append((a, b))
         or_allreduce_(buf, chunk)
 
-    wall, kms = timed_steps(ctx, step, args.steps, args.warmup)
+    wall, kms, phases = timed_steps(ctx, step, args.steps, args.warmup)
     cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
     t0 = time.perf_counter()
     call("vbf_probe_count_dev", vp(keys), None, L, n, 1, m, k, vp(buf), vp(cnt), ctx.sp)
@@ -324,6 +337,7 @@ def main():
     ap.add_argument("--bits-per-key", type=int, default=10)
     ap.add_argument("--neg-keys", type=int, default=None)
     ap.add_argument("--e2e", action="store_true")
+    ap.add_argument("--strategy", type=int, default=0, help="0 auto, 1 atomic, 2 partitioned")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     ap.add_argument("--cpu-opt-threads", type=int, default=16)

@@ -54,6 +54,12 @@ const char* vbf_version(void);
 const char* vbf_last_error(void); /* thread-local; "" when the last call succeeded */
 int vbf_device_count(int* count);
 
+/* Kernel-phase timing with hipEvents on the launch streams (for bench.py's roofline):
+ * phases 0 tile-sort, 1 transpose, 2 segment-OR (partitioned build), 3 atomic build, 4 probe.
+ * vbf_profile_read synchronizes, returns per-phase summed ms and launch counts, and resets. */
+int vbf_profile_enable(int on);
+int vbf_profile_read(double* ms, uint64_t* launches, int nphases);
+
 /* ---- sizing (host arithmetic, glibc log, Rust `as u32` saturation) ---- */
 uint32_t vbf_num_bits(uint64_t n, double p);              /* bf.rs:230-233 */
 uint32_t vbf_num_hash_functions(uint32_t m, uint32_t n);  /* bf.rs:236-239 */
@@ -72,6 +78,22 @@ int vbf_build_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
 int vbf_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                   int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
                   void* stream);
+/* Build strategies.  ATOMIC: one lane per key, k global atomicOr's per key.  PARTITIONED:
+ * hash + per-tile LDS sort by 2^20-bit segment, then one workgroup ORs each segment in LDS
+ * (no global atomics; needs 1 <= k <= 32 and a device workspace the library caches per
+ * stream).  AUTO picks PARTITIONED for batches of >= 2^22 bit indices.  Results are
+ * bit-identical.  vbf_build_dev/_ex expect stream-ordered exclusive use of `words` (the
+ * partitioned path rewrites whole segments); the host and handle APIs merge atomically. */
+#define VBF_BUILD_AUTO 0
+#define VBF_BUILD_ATOMIC 1
+#define VBF_BUILD_PARTITIONED 2
+int vbf_build_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                     int len_prefix, uint32_t m, uint32_t k, uint32_t* words, int strategy,
+                     void* stream);
+/* Device bytes the partitioned build of n keys needs as workspace (0 if unsupported). */
+uint64_t vbf_build_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
+/* Free every cached workspace (synchronizes the streams that own them). */
+int vbf_release_workspaces(void);
 /* Adds the number of keys the filter answers "present" for to *count_dev (device u64). */
 int vbf_probe_count_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                         int len_prefix, uint32_t m, uint32_t k, const uint32_t* words,

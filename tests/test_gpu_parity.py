@@ -48,12 +48,15 @@ def gpu_hashes(vbf, b, k):
     return out.cpu().numpy().view(np.uint64)[: b.n * k].reshape(b.n, k)
 
 
-def gpu_build(vbf, b, m, k, words=None):
+ATOMIC, PARTITIONED = 1, 2
+
+
+def gpu_build(vbf, b, m, k, words=None, strategy=0):
     keys, offs = dev_batch(b)
     nw = (m + 31) // 32
     w = _dev(words.view(np.int32)) if words is not None else torch.zeros(max(nw, 1), dtype=torch.int32, device=DEV)
-    vbf._lib.call("vbf_build_dev", _ptr(keys), _ptr(offs), b.stride, b.n, b.len_prefix, m, k,
-                  _ptr(w), _stream())
+    vbf._lib.call("vbf_build_dev_ex", _ptr(keys), _ptr(offs), b.stride, b.n, b.len_prefix, m, k,
+                  _ptr(w), strategy, _stream())
     torch.cuda.synchronize()
     return w.cpu().numpy().view(np.uint32)[:nw]
 
@@ -111,16 +114,27 @@ def test_hashes_variable_length_unaligned(vbf, ora):
         assert np.array_equal(gpu_hashes(vbf, sb, 3), ora.hashes(b, 3))
 
 
+@pytest.mark.parametrize("strategy", [ATOMIC, PARTITIONED])
 @pytest.mark.parametrize("L,lp,m,k", [(16, 1, 10_000_000, 10), (16, 1, 1, 3), (8, 0, 191701, 19),
                                       (32, 1, 4_000_003, 4), (24, 1, 777_777, 7), (12, 1, 50_000, 5),
-                                      (16, 0, 65536, 33), (100, 1, 1_000_003, 2)])
-def test_build_fixed_matches_oracle(vbf, ora, L, lp, m, k):
+                                      (16, 0, 65536, 32), (100, 1, 1_000_003, 2),
+                                      (16, 1, 3_000_000_017, 1), (16, 1, 4294967295, 4)])
+def test_build_fixed_matches_oracle(vbf, ora, L, lp, m, k, strategy):
     from velarixdb_amd.keys import HostBatch
     n = 200_000 if L <= 32 else 20_000
     data = ora.gen_fixed(0x5EED0001, 0, n, L)
     b = HostBatch(data, None, L, n, lp)
+    if m > 100_000_000:  # sparse check for the huge arrays: compare set bits only
+        got = gpu_build(vbf, b, m, k, strategy=strategy)
+        hs = (ora.hashes(b, k) % np.uint64(m)).ravel()
+        want_idx = np.unique(hs)
+        nz = np.flatnonzero(got)
+        bits = np.unpackbits(got[nz].view(np.uint8), bitorder="little").reshape(-1, 32)
+        got_idx = np.sort((nz[:, None].astype(np.uint64) * np.uint64(32) + np.arange(32, dtype=np.uint64))[bits.astype(bool)])
+        assert np.array_equal(got_idx, want_idx)
+        return
     want = ora.build_words(b, m, k)
-    got = gpu_build(vbf, b, m, k)
+    got = gpu_build(vbf, b, m, k, strategy=strategy)
     assert np.array_equal(got, want)
     # probe: every key present, plus disjoint negatives (j >= n) agree with the oracle
     assert gpu_probe(vbf, b, m, k, got).all()
@@ -142,7 +156,8 @@ def test_config1_bit_exact(vbf, ora):
     assert np.array_equal(gpu_build(vbf, b, m, k), want)
 
 
-def test_build_variable_length_matches_oracle(vbf, ora):
+@pytest.mark.parametrize("strategy", [ATOMIC, PARTITIONED])
+def test_build_variable_length_matches_oracle(vbf, ora, strategy):
     from velarixdb_amd.keys import pack_offsets
     from velarixdb_amd.workloads import SEED_CFG3, SEED_CFG3_NEG, var_offsets
     n, m, k = 100_000, 1_000_003, 10
@@ -150,7 +165,7 @@ def test_build_variable_length_matches_oracle(vbf, ora):
     data = ora.gen_var(SEED_CFG3, 0, off)
     b = pack_offsets(data, off)
     want = ora.build_words(b, m, k)
-    got = gpu_build(vbf, b, m, k)
+    got = gpu_build(vbf, b, m, k, strategy=strategy)
     assert np.array_equal(got, want)
     noff = var_offsets(SEED_CFG3_NEG, 0, 30_000)
     nb = pack_offsets(ora.gen_var(SEED_CFG3_NEG, 0, noff), noff)

@@ -16,6 +16,10 @@ VBF_ENOMEM = -3
 VBF_ENODEV = -4
 VBF_EDIVZERO = -5
 
+VBF_BUILD_AUTO = 0
+VBF_BUILD_ATOMIC = 1
+VBF_BUILD_PARTITIONED = 2
+
 _u8p = ctypes.c_void_p  # raw pointers (host or device) travel as integers
 _u64 = ctypes.c_uint64
 _u32 = ctypes.c_uint32
@@ -28,6 +32,8 @@ SIGNATURES = {
     "vbf_version": (ctypes.c_char_p, []),
     "vbf_last_error": (ctypes.c_char_p, []),
     "vbf_device_count": (_int, [ctypes.POINTER(_int)]),
+    "vbf_profile_enable": (_int, [_int]),
+    "vbf_profile_read": (_int, [_vp, _vp, _int]),
     "vbf_num_bits": (_u32, [_u64, _dbl]),
     "vbf_num_hash_functions": (_u32, [_u32, _u32]),
     "vbf_size": (_int, [_dbl, _u64, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
@@ -35,6 +41,9 @@ SIGNATURES = {
     "vbf_meta_parse": (_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_u32), ctypes.POINTER(_u32),
                               ctypes.POINTER(_dbl)]),
     "vbf_build_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp]),
+    "vbf_build_dev_ex": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _int, _vp]),
+    "vbf_build_workspace_bytes": (_u64, [_u64, _u32, _u32]),
+    "vbf_release_workspaces": (_int, []),
     "vbf_probe_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _vp]),
     "vbf_probe_count_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _vp]),
     "vbf_hashes_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp]),
@@ -103,3 +112,15 @@ def device_count():
     c = _int(0)
     rc = lib.vbf_device_count(ctypes.byref(c))
     return c.value if rc == VBF_OK else 0
+
+
+PHASES = ("tile_sort", "transpose", "seg_or", "atomic_build", "probe")
+
+
+def profile_read():
+    """{phase: (total_ms, launches)} since the last read (needs vbf_profile_enable(1))."""
+    n = len(PHASES)
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_uint64 * n)()
+    call("vbf_profile_read", ms, cnt, n)
+    return {p: (ms[i], cnt[i]) for i, p in enumerate(PHASES)}

@@ -5,7 +5,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["vbf_kernels.hip", "vbf_api.hip"]
+SOURCES = ["vbf_kernels.hip", "vbf_partition.hip", "vbf_api.hip"]
 OUT = os.path.join(HERE, "libvbf.so")
 ARCH = os.environ.get("VBF_OFFLOAD_ARCH", "gfx950")
 
@@ -29,7 +29,7 @@ def needs_build():
 def build(force=False, verbose=False):
     if not force and not needs_build():
         return OUT
-    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++20", "-fPIC", "-shared", "-Wall",
            "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

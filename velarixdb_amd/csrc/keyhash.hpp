@@ -1,0 +1,131 @@
+// keyhash.hpp -- per-key prefix absorption for every key layout the C ABI accepts.
+//
+// key_prefix<FMT, LP>(kb, j) returns the SipHash state after the seed-independent blocks of key
+// j (`LE64(len) || key` when LP), so that h(key, i) = prefix_hash(p, i) costs 5 SipRounds.
+//   FMT  > 0 : fixed length FMT bytes (FMT % 8 == 0), 16-byte (or 8-byte) aligned rows
+//   FMT == 0 : runtime stride
+//   FMT == -1: offsets[n+1], absolute positions into keys
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sip13.hpp"
+
+namespace vbf {
+
+struct DevKeys {
+    const uint8_t* keys;
+    const uint64_t* offsets;
+    uint64_t off_base;
+    uint64_t stride;
+    uint64_t n;
+};
+
+// Aligned 8-byte load of word i of a key whose words start at wstart, or 0 when that word
+// starts at or past `end` (a word holding no key byte is never read: no page can fault).
+__device__ __forceinline__ uint64_t ld_word(const uint64_t* wbase, uintptr_t wstart, uintptr_t end,
+                                            uint64_t i) {
+    return (wstart + 8 * i < end) ? wbase[i] : 0ull;
+}
+
+// The 8 bytes starting `sh` bits into lo:hi (sh in {0, 8, ..., 56}); shift counts stay < 64.
+__device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh) {
+    return (lo >> sh) | ((hi << 1) << (63 - sh));
+}
+
+template <int FMT, bool LP>
+__device__ __forceinline__ Prefix key_prefix(const DevKeys& a, uint64_t j) {
+    Prefix p;
+    if constexpr (FMT > 0) {
+        static_assert(FMT % 8 == 0, "fixed fast path needs whole 8-byte words");
+        constexpr uint32_t NW = FMT / 8;
+        uint64_t w[NW];
+        const uint8_t* kp = a.keys + j * FMT;
+        if constexpr (NW % 2 == 0) {
+#pragma unroll
+            for (uint32_t c = 0; c < NW; c += 2) {
+                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(kp + 8 * c);
+                w[c] = v.x;
+                w[c + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t c = 0; c < NW; ++c) w[c] = *reinterpret_cast<const uint64_t*>(kp + 8 * c);
+        }
+        Sip st = sip_init();
+        if constexpr (LP) sip_compress(st, (uint64_t)FMT);
+#pragma unroll
+        for (uint32_t c = 0; c < NW; ++c) sip_compress(st, w[c]);
+        p.st = st;
+        p.tail = 0;
+        p.r = 0;
+        p.total = (FMT + (LP ? 8 : 0) + 8) & 0xff;
+    } else {
+        uint64_t beg, len;
+        if constexpr (FMT < 0) {
+            beg = a.offsets[j] - a.off_base;
+            len = a.offsets[j + 1] - a.offsets[j];
+        } else {
+            beg = j * a.stride;
+            len = a.stride;
+        }
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(a.keys + beg);
+        const uintptr_t end = addr + len;
+        const uintptr_t wstart = addr & ~(uintptr_t)7;
+        const uint64_t* wbase = reinterpret_cast<const uint64_t*>(wstart);
+        const uint32_t sh = (uint32_t)(addr & 7) * 8;
+        Sip st = sip_init();
+        if constexpr (LP) sip_compress(st, len);
+        const uint64_t nfull = len >> 3;
+        uint64_t lo = len ? ld_word(wbase, wstart, end, 0) : 0ull;
+        for (uint64_t c = 0; c < nfull; ++c) {
+            const uint64_t hi = ld_word(wbase, wstart, end, c + 1);
+            sip_compress(st, funnel(lo, hi, sh));
+            lo = hi;
+        }
+        p.st = st;
+        p.r = (uint32_t)(len & 7);  // P % 8 == len % 8 (the length block is 8 bytes)
+        const uint64_t tmask = p.r ? (~0ull >> (64 - 8 * p.r)) : 0ull;
+        p.tail = p.r ? (funnel(lo, ld_word(wbase, wstart, end, nfull + 1), sh) & tmask) : 0ull;
+        p.total = (uint32_t)((len + (LP ? 8 : 0) + 8) & 0xff);
+    }
+    return p;
+}
+
+// Host-side choice of FMT for a batch: the compile-time fixed layouts need aligned rows.
+enum KeyFmt { kFmtOffsets = -1, kFmtStride = 0 };
+
+inline int pick_fmt(const uint8_t* keys, const uint64_t* offsets, uint64_t stride) {
+    if (offsets) return kFmtOffsets;
+    const uintptr_t k = reinterpret_cast<uintptr_t>(keys);
+    if ((stride == 16 || stride == 32) && (k & 15) == 0) return (int)stride;
+    if ((stride == 8 || stride == 24) && (k & 7) == 0) return (int)stride;
+    return kFmtStride;
+}
+
+// Calls f.template operator()<FMT, LP>() for the batch's layout.
+template <class F>
+inline void with_fmt(int fmt, bool lp, F&& f) {
+#define VBF_FMT_CASE(V)                        \
+    case V:                                    \
+        if (lp)                                \
+            f.template operator()<V, true>();  \
+        else                                   \
+            f.template operator()<V, false>(); \
+        break;
+    switch (fmt) {
+        VBF_FMT_CASE(16)
+        VBF_FMT_CASE(32)
+        VBF_FMT_CASE(8)
+        VBF_FMT_CASE(24)
+        VBF_FMT_CASE(-1)
+        default:
+            if (lp)
+                f.template operator()<0, true>();
+            else
+                f.template operator()<0, false>();
+    }
+#undef VBF_FMT_CASE
+}
+
+}  // namespace vbf

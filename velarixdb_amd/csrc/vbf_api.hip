@@ -94,6 +94,76 @@ vbf::KeyBatch batch(const uint8_t* keys, const uint64_t* offsets, uint64_t off_b
 }
 
 // ---------------------------------------------------------------------------------------
+// Partitioned-build workspace: one grow-only buffer per (device, stream), so concurrent
+// builds on different streams never share scratch.
+// ---------------------------------------------------------------------------------------
+struct Workspace {
+    int device;
+    hipStream_t stream;
+    void* ptr;
+    uint64_t bytes;
+};
+std::mutex g_ws_mu;
+std::vector<Workspace> g_ws;
+
+int get_workspace(hipStream_t s, uint64_t bytes, void** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (auto& w : g_ws) {
+        if (w.device == dev && w.stream == s) {
+            if (w.bytes < bytes) {
+                HIP_TRY(hipStreamSynchronize(s));  // the old buffer may still be in use on s
+                HIP_TRY(hipFree(w.ptr));
+                w.ptr = nullptr;
+                w.bytes = 0;
+                HIP_TRY(hipMalloc(&w.ptr, bytes));
+                w.bytes = bytes;
+            }
+            *out = w.ptr;
+            return VBF_OK;
+        }
+    }
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, bytes));
+    g_ws.push_back(Workspace{dev, s, p, bytes});
+    *out = p;
+    return VBF_OK;
+}
+
+constexpr uint64_t kAutoPartitionMinIdx = 1ull << 22;
+
+// The build every entry point funnels into.  strategy: VBF_BUILD_AUTO / _ATOMIC / _PARTITIONED.
+// atomic_merge: another writer may touch `words` concurrently (the partitioned path then
+// merges its segments with word atomics instead of load+store).
+int do_build(const vbf::KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, int strategy,
+             bool atomic_merge, hipStream_t s) {
+    if (kb.n == 0 || k == 0) return VBF_OK;
+    bool part;
+    if (strategy == VBF_BUILD_ATOMIC) {
+        part = false;
+    } else if (strategy == VBF_BUILD_PARTITIONED) {
+        if (!vbf::partition_supported(m, k))
+            return fail(VBF_EINVAL, "partitioned build needs 1 <= k <= 32 and m > 0 (k = %u)", k);
+        part = true;
+    } else if (strategy == VBF_BUILD_AUTO) {
+        part = vbf::partition_supported(m, k) && kb.n * (uint64_t)k >= kAutoPartitionMinIdx;
+    } else {
+        return fail(VBF_EINVAL, "unknown build strategy %d", strategy);
+    }
+    if (!part) {
+        HIP_TRY(vbf::launch_build(kb, m, k, words, s));
+        return VBF_OK;
+    }
+    const uint64_t need = vbf::partition_workspace_bytes(kb.n, m, k);
+    void* ws = nullptr;
+    int rc = get_workspace(s, need, &ws);
+    if (rc) return rc;
+    HIP_TRY(vbf::launch_build_partitioned(kb, m, k, words, ws, need, atomic_merge, s));
+    return VBF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
 // Host -> device staging: two pinned buffers and two streams per device; chunk c uses
 // buffer (c & 1), so the H2D copy of chunk c+1 overlaps the kernel of chunk c.
 // ---------------------------------------------------------------------------------------
@@ -269,6 +339,40 @@ int new_storage(int device, uint32_t m, std::shared_ptr<Storage>* out) {
     return VBF_OK;
 }
 
+// ---------------------------------------------------------------------------------------
+// Phase profiling: when enabled, every kernel phase is bracketed by hipEvents on its stream.
+// ---------------------------------------------------------------------------------------
+std::atomic<bool> g_prof{false};
+std::mutex g_prof_mu;
+struct PhaseRec {
+    int phase;
+    hipEvent_t a, b;
+};
+std::vector<PhaseRec> g_prof_recs;
+thread_local hipEvent_t g_open[vbf::kNumPhases] = {};
+
+}  // namespace
+
+namespace vbf {
+void phase_begin(int phase, hipStream_t s) {
+    if (!g_prof.load(std::memory_order_relaxed)) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    (void)hipEventRecord(e, s);
+    g_open[phase] = e;
+}
+void phase_end(int phase, hipStream_t s) {
+    if (!g_prof.load(std::memory_order_relaxed) || !g_open[phase]) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    (void)hipEventRecord(e, s);
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_recs.push_back(PhaseRec{phase, g_open[phase], e});
+    g_open[phase] = nullptr;
+}
+}  // namespace vbf
+
+namespace {
 }  // namespace
 
 struct vbf_filter {
@@ -280,7 +384,34 @@ struct vbf_filter {
 
 extern "C" {
 
-const char* vbf_version(void) { return "velarixdb_amd-vbf 0.1.0 gfx950"; }
+const char* vbf_version(void) { return "velarixdb_amd-vbf 0.2.0 gfx950"; }
+
+int vbf_profile_enable(int on) {
+    g_prof.store(on != 0);
+    return ok();
+}
+
+int vbf_profile_read(double* ms, uint64_t* launches, int nphases) {
+    if (!ms || !launches || nphases < 0) return fail(VBF_EINVAL, "NULL argument");
+    for (int i = 0; i < nphases; ++i) {
+        ms[i] = 0.0;
+        launches[i] = 0;
+    }
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (auto& r : g_prof_recs) {
+        float t = 0.f;
+        HIP_TRY(hipEventSynchronize(r.b));
+        HIP_TRY(hipEventElapsedTime(&t, r.a, r.b));
+        if (r.phase < nphases) {
+            ms[r.phase] += t;
+            launches[r.phase] += 1;
+        }
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    g_prof_recs.clear();
+    return ok();
+}
 
 const char* vbf_last_error(void) { return g_err.c_str(); }
 
@@ -342,12 +473,35 @@ int vbf_meta_parse(const uint8_t* in, size_t len, uint32_t* k, uint32_t* n, doub
 
 int vbf_build_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                   int len_prefix, uint32_t m, uint32_t k, uint32_t* words, void* stream) {
+    return vbf_build_dev_ex(keys, offsets, stride, n, len_prefix, m, k, words, VBF_BUILD_AUTO, stream);
+}
+
+uint64_t vbf_build_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
+    return vbf::partition_workspace_bytes(n, m, k);
+}
+
+int vbf_release_workspaces(void) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (auto& w : g_ws) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(w.device);
+        (void)hipStreamSynchronize(w.stream);
+        (void)hipFree(w.ptr);
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    g_ws.clear();
+    return ok();
+}
+
+int vbf_build_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                     int len_prefix, uint32_t m, uint32_t k, uint32_t* words, int strategy, void* stream) {
     int rc = check_mk(m, k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
     if (n && k && !words) return fail(VBF_EINVAL, "words is NULL");
     vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
-    HIP_TRY(vbf::launch_build(kb, m, k, words, (hipStream_t)stream));
+    if ((rc = do_build(kb, m, k, words, strategy, false, (hipStream_t)stream))) return rc;
     return ok();
 }
 
@@ -433,8 +587,7 @@ int vbf_build_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
     rc = pipeline_host_keys(
         *st, keys, offsets, stride, n, len_prefix, false,
         [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t s) -> int {
-            HIP_TRY(vbf::launch_build(kb, m, k, st->d_words, s));
-            return VBF_OK;
+            return do_build(kb, m, k, st->d_words, VBF_BUILD_AUTO, true, s);
         },
         [](int, uint64_t, uint64_t) { return VBF_OK; });
     if (rc) return rc;
@@ -551,7 +704,7 @@ int vbf_filter_set_dev(vbf_filter* f, const uint8_t* keys, const uint64_t* offse
     {
         std::lock_guard<std::mutex> lk(s.mu);
         vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
-        HIP_TRY(vbf::launch_build(kb, s.m, f->k, s.d_words, (hipStream_t)stream));
+        if ((rc = do_build(kb, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, (hipStream_t)stream))) return rc;
     }
     f->n.fetch_add((uint32_t)n);
     return ok();
@@ -576,8 +729,7 @@ int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offs
         rc = pipeline_host_keys(
             *st, keys, offsets, stride, n, len_prefix, false,
             [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t hs) -> int {
-                HIP_TRY(vbf::launch_build(kb, s.m, f->k, s.d_words, hs));
-                return VBF_OK;
+                return do_build(kb, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, hs);
             },
             [](int, uint64_t, uint64_t) { return VBF_OK; });
         if (rc) return rc;

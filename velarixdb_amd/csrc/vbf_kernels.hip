@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "keyhash.hpp"
 #include "sip13.hpp"
 #include "vbf_kernels.hpp"
 
@@ -74,83 +75,14 @@ __device__ __forceinline__ void finish_count(const Args& a, bool hit) {
     }
 }
 
-// ---- fixed-length keys, L % 8 == 0, compile-time L ----
-template <Op OP, uint32_t L, bool LP>
-__global__ __launch_bounds__(kBlock) void k_fixed(Args a) {
+// ---- one lane per key, any layout (keyhash.hpp) ----
+template <Op OP, int FMT, bool LP>
+__global__ __launch_bounds__(kBlock) void k_keys(Args a) {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool hit = false;
     if (j < a.n) {
-        constexpr uint32_t NW = L / 8;
-        uint64_t w[NW];
-        const uint8_t* kp = a.keys + j * L;
-        if constexpr (NW % 2 == 0) {
-#pragma unroll
-            for (uint32_t c = 0; c < NW; c += 2) {
-                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(kp + 8 * c);
-                w[c] = v.x;
-                w[c + 1] = v.y;
-            }
-        } else {
-#pragma unroll
-            for (uint32_t c = 0; c < NW; ++c) w[c] = *reinterpret_cast<const uint64_t*>(kp + 8 * c);
-        }
-        Sip st = sip_init();
-        if constexpr (LP) sip_compress(st, (uint64_t)L);
-#pragma unroll
-        for (uint32_t c = 0; c < NW; ++c) sip_compress(st, w[c]);
-        constexpr uint32_t total = (L + (LP ? 8 : 0) + 8) & 0xff;
-        hit = act<OP>(a, j, [&](uint32_t i) { return prefix_hash_c<0>(st, 0, total, i); });
-    }
-    finish_count<OP>(a, hit);
-}
-
-// Aligned 8-byte load of the word holding key bytes from `wbase + 8*i`, or 0 when that word
-// starts at or past `end` (never touches a word without a valid byte: no page can fault).
-__device__ __forceinline__ uint64_t ld_word(const uint64_t* wbase, uintptr_t wstart, uintptr_t end,
-                                            uint64_t i) {
-    return (wstart + 8 * i < end) ? wbase[i] : 0ull;
-}
-
-// Funnel: the 8 bytes starting `sh` bits into lo (sh in {0,8,...,56}).
-__device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh) {
-    return (lo >> sh) | ((hi << 1) << (63 - sh));
-}
-
-// ---- generic keys: runtime stride or offsets, any length (0 .. MAX_KEY_SIZE and beyond) ----
-template <Op OP, bool OFFS, bool LP>
-__global__ __launch_bounds__(kBlock) void k_generic(Args a) {
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    bool hit = false;
-    if (j < a.n) {
-        uint64_t beg, len;
-        if constexpr (OFFS) {
-            beg = a.offsets[j] - a.off_base;
-            len = a.offsets[j + 1] - a.offsets[j];
-        } else {
-            beg = j * a.stride;
-            len = a.stride;
-        }
-        const uintptr_t addr = reinterpret_cast<uintptr_t>(a.keys + beg);
-        const uintptr_t end = addr + len;
-        const uintptr_t wstart = addr & ~(uintptr_t)7;
-        const uint64_t* wbase = reinterpret_cast<const uint64_t*>(wstart);
-        const uint32_t sh = (uint32_t)(addr & 7) * 8;
-
-        Sip st = sip_init();
-        if constexpr (LP) sip_compress(st, len);
-        const uint64_t nfull = len >> 3;
-        uint64_t lo = len ? ld_word(wbase, wstart, end, 0) : 0ull;
-        for (uint64_t c = 0; c < nfull; ++c) {
-            const uint64_t hi = ld_word(wbase, wstart, end, c + 1);
-            sip_compress(st, funnel(lo, hi, sh));
-            lo = hi;
-        }
-        Prefix p;
-        p.st = st;
-        p.r = (uint32_t)(len & 7);  // P % 8 == len % 8 (the length block is 8 bytes)
-        const uint64_t tmask = p.r ? (~0ull >> (64 - 8 * p.r)) : 0ull;
-        p.tail = p.r ? (funnel(lo, ld_word(wbase, wstart, end, nfull + 1), sh) & tmask) : 0ull;
-        p.total = (uint32_t)((len + (LP ? 8 : 0) + 8) & 0xff);
+        const DevKeys dk{a.keys, a.offsets, a.off_base, a.stride, a.n};
+        const Prefix p = key_prefix<FMT, LP>(dk, j);
         hit = act<OP>(a, j, [&](uint32_t i) { return prefix_hash(p, i); });
     }
     finish_count<OP>(a, hit);
@@ -158,38 +90,12 @@ __global__ __launch_bounds__(kBlock) void k_generic(Args a) {
 
 // ---- host-side dispatch ----
 
-template <Op OP, uint32_t L, bool LP>
-static void launch_fixed(const Args& a, hipStream_t s) {
-    const uint64_t blocks = (a.n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((k_fixed<OP, L, LP>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
-}
-
-template <Op OP, bool OFFS, bool LP>
-static void launch_generic(const Args& a, hipStream_t s) {
-    const uint64_t blocks = (a.n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL((k_generic<OP, OFFS, LP>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
-}
-
-template <Op OP, bool LP>
-static void dispatch_lp(const Args& a, hipStream_t s) {
-    const bool aligned16 = (reinterpret_cast<uintptr_t>(a.keys) & 15) == 0;
-    const bool aligned8 = (reinterpret_cast<uintptr_t>(a.keys) & 7) == 0;
-    if (!a.offsets) {
-        if (a.stride == 16 && aligned16) return launch_fixed<OP, 16, LP>(a, s);
-        if (a.stride == 32 && aligned16) return launch_fixed<OP, 32, LP>(a, s);
-        if (a.stride == 8 && aligned8) return launch_fixed<OP, 8, LP>(a, s);
-        if (a.stride == 24 && aligned8) return launch_fixed<OP, 24, LP>(a, s);
-        return launch_generic<OP, false, LP>(a, s);
-    }
-    return launch_generic<OP, true, LP>(a, s);
-}
-
 template <Op OP>
 static void dispatch(const Args& a, bool lp, hipStream_t s) {
-    if (lp)
-        dispatch_lp<OP, true>(a, s);
-    else
-        dispatch_lp<OP, false>(a, s);
+    const uint64_t blocks = (a.n + kBlock - 1) / kBlock;
+    with_fmt(pick_fmt(a.keys, a.offsets, a.stride), lp, [&]<int FMT, bool LP>() {
+        hipLaunchKernelGGL((k_keys<OP, FMT, LP>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+    });
 }
 
 static Args make_args(const KeyBatch& kb, uint64_t m, uint32_t k) {
@@ -225,33 +131,42 @@ static hipError_t for_chunks(const KeyBatch& kb, F&& f) {
 
 hipError_t launch_build(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, hipStream_t s) {
     if (kb.n == 0 || k == 0) return hipSuccess;
-    return for_chunks<Op::Build>(kb, [&](const KeyBatch& c, uint64_t) {
+    phase_begin(kPhaseAtomicBuild, s);
+    hipError_t e = for_chunks<Op::Build>(kb, [&](const KeyBatch& c, uint64_t) {
         Args a = make_args(c, m, k);
         a.words = words;
         dispatch<Op::Build>(a, c.len_prefix, s);
     });
+    phase_end(kPhaseAtomicBuild, s);
+    return e;
 }
 
 hipError_t launch_probe(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
                         uint8_t* out, hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
-    return for_chunks<Op::Probe>(kb, [&](const KeyBatch& c, uint64_t lo) {
+    phase_begin(kPhaseProbe, s);
+    hipError_t e = for_chunks<Op::Probe>(kb, [&](const KeyBatch& c, uint64_t lo) {
         Args a = make_args(c, m, k);
         a.rwords = words;
         a.out = out + lo;
         dispatch<Op::Probe>(a, c.len_prefix, s);
     });
+    phase_end(kPhaseProbe, s);
+    return e;
 }
 
 hipError_t launch_count(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
                         unsigned long long* count, hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
-    return for_chunks<Op::Count>(kb, [&](const KeyBatch& c, uint64_t) {
+    phase_begin(kPhaseProbe, s);
+    hipError_t e = for_chunks<Op::Count>(kb, [&](const KeyBatch& c, uint64_t) {
         Args a = make_args(c, m, k);
         a.rwords = words;
         a.count = count;
         dispatch<Op::Count>(a, c.len_prefix, s);
     });
+    phase_end(kPhaseProbe, s);
+    return e;
 }
 
 hipError_t launch_hashes(const KeyBatch& kb, uint32_t k, uint64_t* out, hipStream_t s) {

@@ -18,6 +18,20 @@ struct KeyBatch {
 };
 
 hipError_t launch_build(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, hipStream_t s);
+
+// Optional per-phase timing (vbf_profile_*): HIP events recorded on the launch stream.
+enum Phase { kPhaseTileSort = 0, kPhaseTranspose = 1, kPhaseSegOr = 2, kPhaseAtomicBuild = 3,
+             kPhaseProbe = 4, kNumPhases = 5 };
+void phase_begin(int phase, hipStream_t s);
+void phase_end(int phase, hipStream_t s);
+
+// Partitioned build (vbf_partition.hip).  Key batches are processed in chunks of at most
+// kPartChunkIdx bit indices; the workspace holds one chunk's sorted tiles + offset tables.
+constexpr uint64_t kPartChunkIdx = 1ull << 30;
+bool partition_supported(uint32_t m, uint32_t k);
+uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
+hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
+                                    void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s);
 hipError_t launch_probe(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
                         uint8_t* out, hipStream_t s);
 hipError_t launch_count(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
