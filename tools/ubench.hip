@@ -1,0 +1,152 @@
+// ubench.hip -- microbenchmarks that decide the Bloom-build kernel design on gfx950.
+//   hash-*   : SipHash-1-3 prefix + k=10 seeds per lane, XOR-folded (no memory traffic):
+//              variants of the 64-bit rotate / add lowering.
+//   atomic   : random 32-bit atomicOr rate into arrays of several sizes.
+//   gather   : random 32-bit load rate from the same arrays.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 -o tools/ubench tools/ubench.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#define CHECK(x)                                                                       \
+    do {                                                                               \
+        hipError_t e = (x);                                                            \
+        if (e != hipSuccess) {                                                         \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                     \
+            return 1;                                                                  \
+        }                                                                              \
+    } while (0)
+
+struct S { uint64_t v0, v1, v2, v3; };
+
+// V0: plain C rotates (compiler picks v_lshlrev_b64 + v_lshrrev + v_or)
+__device__ __forceinline__ uint64_t rotl_c(uint64_t x, int b) { return (x << b) | (x >> (64 - b)); }
+// V1: v_alignbit_b32 pair
+template <int B>
+__device__ __forceinline__ uint64_t rotl_a(uint64_t x) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - B);
+    const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - B);
+    return ((uint64_t)nhi << 32) | nlo;
+}
+__device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x >> 32) | (x << 32); }
+// 64-bit add as add_co/addc through inline asm (defeats v_lshl_add_u64 selection)
+__device__ __forceinline__ uint64_t add_cc(uint64_t a, uint64_t b) {
+    uint32_t lo, hi;
+    asm volatile("v_add_co_u32 %0, vcc, %2, %3\n\tv_addc_co_u32 %1, vcc, %4, %5, vcc"
+                 : "=v"(lo), "=v"(hi)
+                 : "v"((uint32_t)a), "v"((uint32_t)b), "v"((uint32_t)(a >> 32)), "v"((uint32_t)(b >> 32))
+                 : "vcc");
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int V>
+__device__ __forceinline__ void round_(S& s) {
+    if constexpr (V == 0) {
+        s.v0 += s.v1; s.v1 = rotl_c(s.v1, 13); s.v1 ^= s.v0; s.v0 = rotl_c(s.v0, 32);
+        s.v2 += s.v3; s.v3 = rotl_c(s.v3, 16); s.v3 ^= s.v2;
+        s.v0 += s.v3; s.v3 = rotl_c(s.v3, 21); s.v3 ^= s.v0;
+        s.v2 += s.v1; s.v1 = rotl_c(s.v1, 17); s.v1 ^= s.v2; s.v2 = rotl_c(s.v2, 32);
+    } else if constexpr (V == 1) {
+        s.v0 += s.v1; s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap32(s.v0);
+        s.v2 += s.v3; s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
+        s.v0 += s.v3; s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
+        s.v2 += s.v1; s.v1 = rotl_a<17>(s.v1); s.v1 ^= s.v2; s.v2 = swap32(s.v2);
+    } else {
+        s.v0 = add_cc(s.v0, s.v1); s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap32(s.v0);
+        s.v2 = add_cc(s.v2, s.v3); s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
+        s.v0 = add_cc(s.v0, s.v3); s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
+        s.v2 = add_cc(s.v2, s.v1); s.v1 = rotl_a<17>(s.v1); s.v1 ^= s.v2; s.v2 = swap32(s.v2);
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void comp(S& s, uint64_t m) { s.v3 ^= m; round_<V>(s); s.v0 ^= m; }
+
+template <int V>
+__device__ __forceinline__ uint64_t fin(S s, uint64_t b) {
+    s.v3 ^= b; round_<V>(s); s.v0 ^= b; s.v2 ^= 0xff; round_<V>(s); round_<V>(s); round_<V>(s);
+    return s.v0 ^ s.v1 ^ s.v2 ^ s.v3;
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void k_hash(uint64_t n, int k, uint64_t* out) {
+    uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    S s{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL, 0x7465646279746573ULL};
+    comp<V>(s, 16); comp<V>(s, j * 0x9E3779B97F4A7C15ULL); comp<V>(s, j);
+    uint64_t acc = 0;
+    for (int i = 0; i < k; ++i) {
+        S t = s;
+        comp<V>(t, (uint64_t)i);
+        acc ^= fin<V>(t, 32ull << 56);
+    }
+    if (acc == 0x123456789ull) out[0] = acc;  // keep it live, never taken in practice
+}
+
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+__global__ __launch_bounds__(256) void k_atomic(uint32_t* w, uint32_t nw, uint64_t n, int per) {
+    uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    for (int i = 0; i < per; ++i) {
+        uint32_t h = mix32(j * 16 + i);
+        atomicOr(w + (h % nw), 1u << (h & 31));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gather(const uint32_t* w, uint32_t nw, uint64_t n, int per, uint32_t* out) {
+    uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    uint32_t acc = 0;
+    for (int i = 0; i < per; ++i) {
+        uint32_t h = mix32(j * 16 + i);
+        acc += w[h % nw];
+    }
+    if (acc == 0xdeadbeef) out[0] = acc;
+}
+
+template <class F>
+static float time_ms(F&& f, int reps) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+    f();
+    (void)hipDeviceSynchronize();
+    (void)hipEventRecord(a, 0);
+    for (int r = 0; r < reps; ++r) f();
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0; (void)hipEventElapsedTime(&ms, a, b);
+    return ms / reps;
+}
+
+int main() {
+    const uint64_t n = 100000000;
+    uint64_t* out;
+    CHECK(hipMalloc(&out, 8));
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    float t0 = time_ms([&] { hipLaunchKernelGGL(k_hash<0>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
+    float t1 = time_ms([&] { hipLaunchKernelGGL(k_hash<1>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
+    float t2 = time_ms([&] { hipLaunchKernelGGL(k_hash<2>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
+    printf("hash 100M keys x k=10 (53 SipRounds/key): V0 shifts %.3f ms  V1 alignbit %.3f ms  V2 alignbit+addc %.3f ms\n",
+           t0, t1, t2);
+    printf("  -> G SipRounds/s: V0 %.1f  V1 %.1f  V2 %.1f\n", 53e8 / t0 / 1e6, 53e8 / t1 / 1e6, 53e8 / t2 / 1e6);
+    uint32_t* w;
+    const uint64_t maxw = 1ull << 29;  // 2 GiB
+    CHECK(hipMalloc(&w, maxw * 4));
+    CHECK(hipMemset(w, 0, maxw * 4));
+    uint32_t* o32;
+    CHECK(hipMalloc(&o32, 4));
+    const uint64_t na = 100000000;
+    for (uint64_t mb : {1ull, 4ull, 32ull, 125ull, 512ull, 2048ull}) {
+        const uint32_t nw = (uint32_t)(mb * (1ull << 20) / 4);
+        float ta = time_ms([&] { hipLaunchKernelGGL(k_atomic, dim3((unsigned)((na + 255) / 256)), dim3(256), 0, 0, w, nw, na, 10); }, 3);
+        float tg = time_ms([&] { hipLaunchKernelGGL(k_gather, dim3((unsigned)((na + 255) / 256)), dim3(256), 0, 0, w, nw, na, 10, o32); }, 3);
+        printf("array %5llu MiB: random atomicOr %.1f G/s   random load %.1f G/s\n", (unsigned long long)mb,
+               na * 10 / ta / 1e6, na * 10 / tg / 1e6);
+    }
+    return 0;
+}
