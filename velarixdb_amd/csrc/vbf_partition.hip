@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "keyhash.hpp"
 #include "sip13.hpp"
@@ -29,13 +30,13 @@
 namespace vbf {
 
 constexpr int kPBlock = 1024;      // threads per K1 / K3 workgroup
-constexpr int kStash = 32;         // bit indices a lane keeps in registers
+constexpr int kStash = 32;         // max bit indices a lane keeps in registers (k <= kStash)
 constexpr int kSegBits = 20;       // segment = 2^20 bits = 128 KiB of LDS
 constexpr uint32_t kSegWords = 1u << (kSegBits - 5);
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a bit index: idx < m <= 2^32 - 1
 
 struct PartPlan {
-    uint32_t k, R, KT, C, nseg, G;
+    uint32_t k, KS, R, KT, C, nseg, G;
     uint64_t m, mu, nwords;
 };
 
@@ -78,9 +79,11 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
     }
 }
 
-template <int FMT, bool LP>
-__global__ __launch_bounds__(kPBlock) void k_tile_sort(DevKeys dk, PartPlan pl, uint32_t* tiles,
-                                                       uint16_t* ends) {
+// KS = stash slots per lane: 32 -> one 1024-thread workgroup per CU (big tiles, long runs);
+// 16 -> two per CU (8 waves/SIMD for the hashing, shorter runs).
+template <int FMT, bool LP, int KS>
+__global__ __launch_bounds__(kPBlock, KS == 16 ? 8 : 4) void k_tile_sort(DevKeys dk, PartPlan pl,
+                                                                         uint32_t* tiles, uint16_t* ends) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* sorted = smem;            // C entries
     uint32_t* cnt = smem + pl.C;        // nseg entries (+ pad)
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_sort(DevKeys dk, PartPlan pl, 
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
     __syncthreads();
 
-    uint32_t stash[kStash];
+    uint32_t stash[KS];
     uint32_t ns = 0;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
     for (uint32_t r = 0; r < pl.R; ++r) {
@@ -142,6 +145,10 @@ __global__ __launch_bounds__(256) void k_transpose_u16(const uint16_t* in, uint1
     }
 }
 
+// One lane per (tile, segment) run: a lane walks its run with 16-byte loads (4-byte aligned:
+// gfx950 global loads need only dword alignment), four loads in flight before their ds_or's,
+// so each wave keeps 64 runs x 64 bytes of loads outstanding.  Words past a run's end belong to
+// the next run of the same tile (or to the workspace's 64-byte tail pad) and are masked off.
 __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const uint16_t* endsT,
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
                                                     uint32_t* words) {
@@ -151,27 +158,44 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     const uint64_t wbase = (uint64_t)seg * kSegWords;
     const uint32_t wn = (uint32_t)std::min<uint64_t>(kSegWords, pl.nwords - wbase);
     const bool own = (pl.G == 1) && !atomic_merge;  // sole writer: start from the existing words
-    for (uint32_t w = tid; w < kSegWords; w += kPBlock) bitmap[w] = (own && w < wn) ? words[wbase + w] : 0u;
+    for (uint32_t w = tid * 4; w < kSegWords; w += kPBlock * 4) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (own) {
+            if (w + 4 <= wn)
+                v = *reinterpret_cast<const uint4*>(words + wbase + w);
+            else if (w < wn) {
+                v.x = words[wbase + w];
+                if (w + 1 < wn) v.y = words[wbase + w + 1];
+                if (w + 2 < wn) v.z = words[wbase + w + 2];
+            }
+        }
+        *reinterpret_cast<uint4*>(bitmap + w) = v;
+    }
     __syncthreads();
 
     const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / pl.G);
     const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / pl.G);
     const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
     const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * ntiles : nullptr;
-    const uint32_t half = lane >> 5, hl = lane & 31;
-    for (uint32_t tg = t_lo + wave * 64; tg < t_hi; tg += (kPBlock / 64) * 64) {
-        const uint32_t t = tg + lane;
+    for (uint32_t t = t_lo + wave * 64 + lane; t - lane < t_hi; t += kPBlock) {
         uint32_t st = 0, en = 0;
         if (t < t_hi) {
             st = row_beg ? row_beg[t] : 0;
             en = row_end[t];
         }
-        for (uint32_t q = 0; q < 64; q += 2) {
-            const uint32_t s_q = __shfl(st, q + half), e_q = __shfl(en, q + half);
-            const uint32_t* base = tiles + (uint64_t)(tg + q + half) * pl.C;
-            for (uint32_t e = s_q + hl; e < e_q; e += 32) {
-                const uint32_t idx = base[e];
-                atomicOr(&bitmap[(idx >> 5) & (kSegWords - 1)], 1u << (idx & 31));
+        const uint32_t* run = tiles + (uint64_t)t * pl.C;
+        for (uint32_t e = st; e < en; e += 16) {
+            uint4 v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (e + 4 * q < en) __builtin_memcpy(&v[q], run + e + 4 * q, 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t b = e + 4 * q;
+                const uint32_t x[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    if (b + c < en) atomicOr(&bitmap[(x[c] >> 5) & (kSegWords - 1)], 1u << (x[c] & 31));
             }
         }
     }
@@ -191,10 +215,20 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     }
 }
 
+static uint32_t stash_slots(uint32_t k) {
+    static const int env = [] {
+        const char* e = getenv("VBF_TILE_KS");
+        return e ? atoi(e) : 0;
+    }();
+    if (env == 16 && k <= 16) return 16;
+    return 32;
+}
+
 static PartPlan make_plan(uint32_t m, uint32_t k) {
     PartPlan pl{};
     pl.k = k;
-    pl.R = kStash / k;
+    pl.KS = stash_slots(k);
+    pl.R = pl.KS / k;
     pl.KT = pl.R * kPBlock;
     pl.C = pl.KT * k;
     pl.m = m;
@@ -212,7 +246,7 @@ uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     const PartPlan pl = make_plan(m, k);
     uint64_t chunk_keys = std::min<uint64_t>(n, kPartChunkIdx / k);
     const uint64_t ntiles = (chunk_keys + pl.KT - 1) / pl.KT;
-    return ntiles * ((uint64_t)pl.C * 4 + (uint64_t)pl.nseg * 4) + 256;
+    return ntiles * ((uint64_t)pl.C * 4 + (uint64_t)pl.nseg * 4) + 512;
 }
 
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
@@ -239,7 +273,7 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         hipError_t err = hipSuccess;
         phase_begin(kPhaseTileSort, s);
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
-            auto fn = k_tile_sort<FMT, LP>;
+            auto fn = pl.KS == 16 ? k_tile_sort<FMT, LP, 16> : k_tile_sort<FMT, LP, 32>;
             err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
             if (err == hipSuccess)
