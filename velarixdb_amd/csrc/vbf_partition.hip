@@ -112,9 +112,17 @@ __global__ __launch_bounds__(kPBlock, KS == 16 ? 8 : 4) void k_tile_sort(DevKeys
     __syncthreads();
     block_exclusive_scan(cnt, pl.nseg, wsum);
     __syncthreads();
-    for (uint32_t t = 0; t < ns; ++t) {
-        const uint32_t idx = stash[t];
-        if (idx != kSentinel) sorted[atomicAdd(&cnt[idx >> kSegBits], 1u)] = idx;
+    // rank + place, 8 returning LDS atomics in flight before their results are used
+    for (uint32_t t = 0; t < ns; t += 8) {
+        uint32_t pos[8], val[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
+            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> kSegBits], 1u) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (val[q] != kSentinel) sorted[pos[q]] = val[q];
     }
     __syncthreads();
     // cnt[s] now holds the end of segment s's run within the sorted tile
@@ -145,10 +153,12 @@ __global__ __launch_bounds__(256) void k_transpose_u16(const uint16_t* in, uint1
     }
 }
 
-// One lane per (tile, segment) run: a lane walks its run with 16-byte loads (4-byte aligned:
-// gfx950 global loads need only dword alignment), four loads in flight before their ds_or's,
-// so each wave keeps 64 runs x 64 bytes of loads outstanding.  Words past a run's end belong to
-// the next run of the same tile (or to the workspace's 64-byte tail pad) and are masked off.
+// Runs are read by 8-lane groups: lane q of a group loads words [4q, 4q+4) and [32+4q, 32+4q+4)
+// of its run with 16-byte loads (4-byte aligned: gfx950 global loads need only dword alignment),
+// so one wave instruction covers 8 runs x 128 contiguous bytes.  All 16 loads of the 64 runs a
+// wave owns are issued before the first ds_or; the few runs longer than 64 words finish in a
+// tail loop.  Words past a run's end belong to the next run of the same tile (or to the
+// workspace's tail pad) and are masked off.
 __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const uint16_t* endsT,
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
                                                     uint32_t* words) {
@@ -177,25 +187,48 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / pl.G);
     const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
     const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * ntiles : nullptr;
-    for (uint32_t t = t_lo + wave * 64 + lane; t - lane < t_hi; t += kPBlock) {
-        uint32_t st = 0, en = 0;
-        if (t < t_hi) {
-            st = row_beg ? row_beg[t] : 0;
-            en = row_end[t];
+    const uint32_t grp = lane >> 3, q4 = (lane & 7) * 4;
+    for (uint32_t tg = t_lo + wave * 64; tg < t_hi; tg += kPBlock) {
+        // element offsets fit u32: one chunk holds < 2^30 + C indices (kPartChunkIdx)
+        uint32_t off[8], len[8];
+        uint4 d0[8], d1[8];
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            const uint32_t t = tg + g * 8 + grp;  // the 8 lanes of a group read the same u16
+            uint32_t st = 0, en = 0;
+            if (t < t_hi) {
+                st = row_beg ? row_beg[t] : 0;
+                en = row_end[t];
+            }
+            off[g] = t * pl.C + st + q4;
+            len[g] = en - st;
         }
-        const uint32_t* run = tiles + (uint64_t)t * pl.C;
-        for (uint32_t e = st; e < en; e += 16) {
-            uint4 v[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (e + 4 * q < en) __builtin_memcpy(&v[q], run + e + 4 * q, 16);
+        for (int g = 0; g < 8; ++g) {
+            if (q4 < len[g]) __builtin_memcpy(&d0[g], tiles + off[g], 16);
+            if (q4 + 32 < len[g]) __builtin_memcpy(&d1[g], tiles + off[g] + 32, 16);
+        }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t b = e + 4 * q;
-                const uint32_t x[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+        for (int g = 0; g < 8; ++g) {
+            const uint32_t a[4] = {d0[g].x, d0[g].y, d0[g].z, d0[g].w};
+            const uint32_t b[4] = {d1[g].x, d1[g].y, d1[g].z, d1[g].w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (q4 + c < len[g]) atomicOr(&bitmap[(a[c] >> 5) & (kSegWords - 1)], 1u << (a[c] & 31));
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (q4 + 32 + c < len[g]) atomicOr(&bitmap[(b[c] >> 5) & (kSegWords - 1)], 1u << (b[c] & 31));
+        }
+        // tail: runs longer than 64 words (rare at the default plan; common for tiny m)
+#pragma unroll 1
+        for (int g = 0; g < 8; ++g) {
+            for (uint32_t e = q4 + 64; e < len[g]; e += 32) {
+                uint4 v;
+                __builtin_memcpy(&v, tiles + off[g] - q4 + e, 16);
+                const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    if (b + c < en) atomicOr(&bitmap[(x[c] >> 5) & (kSegWords - 1)], 1u << (x[c] & 31));
+                    if (e + c < len[g]) atomicOr(&bitmap[(x[c] >> 5) & (kSegWords - 1)], 1u << (x[c] & 31));
             }
         }
     }
