@@ -136,6 +136,57 @@ __global__ __launch_bounds__(kPBlock, KS == 16 ? 8 : 4) void k_tile_sort(DevKeys
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)cnt[s];
 }
 
+// Same tile contract, no LDS copy of the tile: each index is stored straight to its sorted slot
+// in the tile's global region (the block's 120 KiB of scattered 4-byte stores land in L2 within
+// a few microseconds and leave as whole lines).  LDS holds only the counters, so two
+// 1024-thread workgroups fit per CU (8 waves/SIMD for the hashing).
+template <int FMT, bool LP>
+__global__ __launch_bounds__(kPBlock) void k_tile_sort_direct(DevKeys dk, PartPlan pl, uint32_t* tiles,
+                                                                 uint16_t* ends) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t* cnt = smem;  // nseg entries (+ pad)
+    uint32_t* wsum = cnt + ((pl.nseg + 3) & ~3u);
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
+    __syncthreads();
+
+    uint32_t stash[kStash];
+    uint32_t ns = 0;
+    const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
+    for (uint32_t r = 0; r < pl.R; ++r) {
+        const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
+        const bool valid = j < dk.n;
+        Prefix p{};
+        if (valid) p = key_prefix<FMT, LP>(dk, j);
+        for (uint32_t i = 0; i < pl.k; ++i) {
+            uint32_t idx = kSentinel;
+            if (valid) {
+                idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
+                atomicAdd(&cnt[idx >> kSegBits], 1u);
+            }
+            stash[ns++] = idx;
+        }
+    }
+    __syncthreads();
+    block_exclusive_scan(cnt, pl.nseg, wsum);
+    __syncthreads();
+    uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.C;
+    for (uint32_t t = 0; t < ns; t += 8) {
+        uint32_t pos[8], val[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
+            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> kSegBits], 1u) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (val[q] != kSentinel) out[pos[q]] = val[q];
+    }
+    __syncthreads();
+    uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nseg;
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)cnt[s];
+}
+
 // ends[rows][cols] -> endsT[cols][rows], 64x64 tiles through LDS.
 __global__ __launch_bounds__(256) void k_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows,
                                                        uint32_t cols) {
@@ -248,13 +299,21 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     }
 }
 
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 static uint32_t stash_slots(uint32_t k) {
-    static const int env = [] {
-        const char* e = getenv("VBF_TILE_KS");
-        return e ? atoi(e) : 0;
-    }();
+    static const int env = env_int("VBF_TILE_KS", 0);
     if (env == 16 && k <= 16) return 16;
     return 32;
+}
+
+// K1 variant: 0 = LDS-sorted tile copy, 1 = direct scattered stores (VBF_TILE_DIRECT)
+static int tile_direct() {
+    static const int env = env_int("VBF_TILE_DIRECT", 0);
+    return env;
 }
 
 static PartPlan make_plan(uint32_t m, uint32_t k) {
@@ -294,7 +353,8 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
     uint16_t* ends = reinterpret_cast<uint16_t*>(tiles + max_tiles * pl.C);
     uint16_t* endsT = ends + max_tiles * pl.nseg;
 
-    const size_t lds1 = ((size_t)pl.C + ((pl.nseg + 3) & ~3u) + 64) * 4;
+    const bool direct = tile_direct() && pl.KS == 32;
+    const size_t lds1 = ((size_t)(direct ? 0 : pl.C) + ((pl.nseg + 3) & ~3u) + 64) * 4;
     for (uint64_t lo = 0; lo < kb.n; lo += chunk_keys) {
         const uint64_t cn = std::min<uint64_t>(chunk_keys, kb.n - lo);
         DevKeys dk{kb.keys, kb.offsets, kb.off_base, kb.stride, cn};
@@ -306,7 +366,8 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         hipError_t err = hipSuccess;
         phase_begin(kPhaseTileSort, s);
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
-            auto fn = pl.KS == 16 ? k_tile_sort<FMT, LP, 16> : k_tile_sort<FMT, LP, 32>;
+            auto fn = direct ? k_tile_sort_direct<FMT, LP>
+                             : pl.KS == 16 ? k_tile_sort<FMT, LP, 16> : k_tile_sort<FMT, LP, 32>;
             err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
             if (err == hipSuccess)
