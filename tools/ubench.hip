@@ -40,6 +40,16 @@ __device__ __forceinline__ uint64_t add_cc(uint64_t a, uint64_t b) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// 64-bit add as add_co/addc through non-volatile asm (schedulable)
+__device__ __forceinline__ uint64_t add_nv(uint64_t a, uint64_t b) {
+    uint32_t lo, hi;
+    asm("v_add_co_u32 %0, vcc, %2, %3\n\tv_addc_co_u32 %1, vcc, %4, %5, vcc"
+        : "=&v"(lo), "=v"(hi)
+        : "v"((uint32_t)a), "v"((uint32_t)b), "v"((uint32_t)(a >> 32)), "v"((uint32_t)(b >> 32))
+        : "vcc");
+    return ((uint64_t)hi << 32) | lo;
+}
+
 template <int V>
 __device__ __forceinline__ void round_(S& s) {
     if constexpr (V == 0) {
@@ -52,6 +62,11 @@ __device__ __forceinline__ void round_(S& s) {
         s.v2 += s.v3; s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
         s.v0 += s.v3; s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
         s.v2 += s.v1; s.v1 = rotl_a<17>(s.v1); s.v1 ^= s.v2; s.v2 = swap32(s.v2);
+    } else if constexpr (V == 3) {
+        s.v0 = add_nv(s.v0, s.v1); s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap32(s.v0);
+        s.v2 = add_nv(s.v2, s.v3); s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
+        s.v0 = add_nv(s.v0, s.v3); s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
+        s.v2 = add_nv(s.v2, s.v1); s.v1 = rotl_a<17>(s.v1); s.v1 ^= s.v2; s.v2 = swap32(s.v2);
     } else {
         s.v0 = add_cc(s.v0, s.v1); s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap32(s.v0);
         s.v2 = add_cc(s.v2, s.v3); s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
@@ -82,6 +97,45 @@ __global__ __launch_bounds__(256) void k_hash(uint64_t n, int k, uint64_t* out) 
         acc ^= fin<V>(t, 32ull << 56);
     }
     if (acc == 0x123456789ull) out[0] = acc;  // keep it live, never taken in practice
+}
+
+__device__ __forceinline__ uint32_t fmod_(uint64_t x, uint64_t m, uint64_t mu) {
+    const uint64_t q = __umul64hi(x, mu);
+    uint64_t r = x - q * m;
+    r = r >= m ? r - m : r;
+    return (uint32_t)r;
+}
+
+// MODE: 0 = V1 hash only; 1 = V1 + mod; 2 = V1, two seeds interleaved, + mod; 3 = V3 + mod
+template <int MODE, int BS>
+__global__ __launch_bounds__(BS) void k_hash2(uint64_t n, int k, uint64_t m, uint64_t mu, uint64_t* out) {
+    extern __shared__ uint32_t pad[];
+    uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
+    if (j >= n) return;
+    constexpr int V = MODE == 3 ? 3 : 1;
+    S s{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL, 0x7465646279746573ULL};
+    comp<V>(s, 16); comp<V>(s, j * 0x9E3779B97F4A7C15ULL); comp<V>(s, j);
+    uint64_t acc = 0;
+    if constexpr (MODE == 2) {
+        int i = 0;
+        for (; i + 1 < k; i += 2) {
+            S t0 = s, t1 = s;
+            comp<V>(t0, (uint32_t)i);
+            comp<V>(t1, (uint32_t)(i + 1));
+            const uint64_t h0 = fin<V>(t0, 32ull << 56);
+            const uint64_t h1 = fin<V>(t1, 32ull << 56);
+            acc += fmod_(h0, m, mu) + fmod_(h1, m, mu);
+        }
+        if (i < k) { S t = s; comp<V>(t, (uint32_t)i); acc += fmod_(fin<V>(t, 32ull << 56), m, mu); }
+    } else {
+        for (int i = 0; i < k; ++i) {
+            S t = s;
+            comp<V>(t, (uint32_t)i);
+            const uint64_t h = fin<V>(t, 32ull << 56);
+            if constexpr (MODE == 0) acc ^= h; else acc += fmod_(h, m, mu);
+        }
+    }
+    if (acc == 0x123456789ull) out[0] = acc + pad[0];
 }
 
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {
@@ -134,6 +188,22 @@ int main() {
     printf("hash 100M keys x k=10 (53 SipRounds/key): V0 shifts %.3f ms  V1 alignbit %.3f ms  V2 alignbit+addc %.3f ms\n",
            t0, t1, t2);
     printf("  -> G SipRounds/s: V0 %.1f  V1 %.1f  V2 %.1f\n", 53e8 / t0 / 1e6, 53e8 / t1 / 1e6, 53e8 / t2 / 1e6);
+    {
+        const uint64_t m = 1000000000ull, mu = ~0ull / m;
+        auto run = [&](auto kern, int bs, size_t lds, const char* name) {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            float t = time_ms([&] { hipLaunchKernelGGL(kern, dim3((unsigned)((n + bs - 1) / bs)), dim3(bs), lds, 0, n, 10, m, mu, out); }, 5);
+            printf("  %-44s %.3f ms\n", name, t);
+        };
+        printf("hash variants, 100M keys x k=10 (m = 1e9):\n");
+        run(k_hash2<0, 256>, 256, 0, "V1 hash only, 256 thr");
+        run(k_hash2<1, 256>, 256, 0, "V1 + mod, 256 thr");
+        run(k_hash2<2, 256>, 256, 0, "V1 2-seed interleave + mod, 256 thr");
+        run(k_hash2<3, 256>, 256, 0, "V3 addc + mod, 256 thr");
+        run(k_hash2<1, 1024>, 1024, 120 * 1024, "V1 + mod, 1024 thr, 1 block/CU (LDS)");
+        run(k_hash2<2, 1024>, 1024, 120 * 1024, "V1 2-seed + mod, 1024 thr, 1 block/CU");
+        run(k_hash2<3, 1024>, 1024, 120 * 1024, "V3 addc + mod, 1024 thr, 1 block/CU");
+    }
     uint32_t* w;
     const uint64_t maxw = 1ull << 29;  // 2 GiB
     CHECK(hipMalloc(&w, maxw * 4));
