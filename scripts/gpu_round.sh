@@ -25,11 +25,8 @@ for s in $STEPS; do
   case $s in
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest_gpu 1200 python -m pytest tests -x -q -m gpu ;;
-    pytestdirect) run pytest_gpu_direct 1200 env VBF_TILE_DIRECT=1 python -m pytest tests -x -q -m gpu -k "build or config or partition or sst" ;;
     bench)  run bench 600 python bench.py ;;
     benchq)  run bench_quick 300 python bench.py --no-cpu-baseline ;;
-    benchks16) run bench_ks16 300 env VBF_TILE_KS=16 python bench.py --no-cpu-baseline ;;
-    benchdirect) run bench_direct 300 env VBF_TILE_DIRECT=1 python bench.py --no-cpu-baseline ;;
     benchatomic) run bench_atomic 300 python bench.py --no-cpu-baseline --strategy 1 --steps 3 ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
     bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;

@@ -1,22 +1,26 @@
 // vbf_partition.hip -- the partitioned Bloom build: no global atomics on the hot path.
 //
-// Random `atomicOr`s into a 125 MB bit array run at the memory-side atomic rate (~27 G/s on
-// MI355X, measured: profiles/r01), 1e9 of them per 100M-key build.  Instead:
+// Random `atomicOr`s into a 125 MB bit array run at the memory-side atomic rate (27 G/s on
+// MI355X whatever the array size, tools/ubench), 1e9 of them per 100M-key build.  Instead:
 //
-//   K1 k_tile_sort : one 1024-thread workgroup per tile of R*1024 keys.  Each lane hashes its
-//                    keys (k SipHash-1-3 per key, shared prefix), keeps the k bit indices in
-//                    registers (stash), counts them per 2^20-bit segment in LDS, scans the
-//                    counts, scatters the indices into an LDS copy of the tile sorted by
-//                    segment, and writes that copy out with coalesced stores, plus the tile's
-//                    per-segment end offsets (u16).
+//   K1 k_tile_pack : one 1024-thread workgroup per tile of KT keys, two workgroups per CU.  Each
+//                    lane hashes its keys (k SipHash-1-3 per key over a shared prefix) and keeps
+//                    the k bit indices in registers; the workgroup counts them per 2^20-bit
+//                    segment in LDS, scans the counts, and places every index into an LDS copy
+//                    of the tile sorted by segment.  The copy is PACKED: an index inside its
+//                    segment is 20 bits, stored as a u16 low half plus a 4-bit nibble (2.5 B per
+//                    index instead of 4), and every segment's run is padded to an even length
+//                    (by repeating one of its indices: OR is idempotent) so that K3's loads stay
+//                    dword-aligned.  The tile and its per-segment run ends (u16) are written
+//                    out with coalesced stores.
 //   K2 k_transpose : ends[tile][seg] -> endsT[seg][tile] so each segment reads one row.
-//   K3 k_seg_or    : one workgroup per 2^20-bit segment (128 KiB of LDS): gathers that
-//                    segment's run from every tile, ORs the bits into LDS with ds_or, then
-//                    writes the segment's 32768 words with coalesced stores (or merges them
-//                    with word-wise atomics when several workgroups share a segment).
+//   K3 k_seg_or    : one workgroup per segment (128 KiB of LDS): 8-lane groups read that
+//                    segment's run from every tile with 16-byte loads, all issued before the
+//                    first ds_or, then the segment's 32768 words are written with coalesced
+//                    stores (or merged with word atomics when several workgroups share it).
 //
-// Results are bit-identical to the per-key atomic kernel (OR is order-independent); the
-// build still ORs into the existing words (bf.rs:89 never clears bits).
+// Results are bit-identical to the per-key atomic kernel (OR is order-independent); the build
+// ORs into the existing words (bf.rs:89 never clears bits).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,18 +33,26 @@
 
 namespace vbf {
 
-constexpr int kPBlock = 1024;      // threads per K1 / K3 workgroup
-constexpr int kStash = 32;         // max bit indices a lane keeps in registers (k <= kStash)
-constexpr int kSegBits = 20;       // segment = 2^20 bits = 128 KiB of LDS
+constexpr int kPBlock = 1024;                // threads per K1 / K3 workgroup
+constexpr int kStash = 32;                   // max bit indices a lane keeps in registers
+constexpr int kSegBits = 20;                 // segment = 2^20 bits = 128 KiB of LDS
 constexpr uint32_t kSegWords = 1u << (kSegBits - 5);
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a bit index: idx < m <= 2^32 - 1
+constexpr uint32_t kLdsPerCu = 163840;
 
 struct PartPlan {
-    uint32_t k, KS, R, KT, C, nseg, G;
+    uint32_t k;
+    uint32_t R;           // hashing rounds per lane (ceil(KT / 1024))
+    uint32_t KT;          // keys per tile
+    uint32_t C;           // indices per tile (KT * k)
+    uint32_t CP;          // padded capacity: C + nseg, rounded up to a multiple of 8
+    uint32_t nseg, nseg_pad, G;
+    uint32_t tile_words;  // u32 words per tile in the workspace: CP/2 (lo16) + CP/8 (nibbles)
+    uint32_t lds1;        // K1 dynamic LDS bytes
     uint64_t m, mu, nwords;
 };
 
-// Exclusive scan of v[0..n) in LDS (n <= 4 * kPBlock); returns nothing, v holds the prefix.
+// Exclusive scan of v[0..n) in LDS (n <= 4 * kPBlock).
 __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, uint32_t* wsum) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t loc[4];
@@ -60,14 +72,14 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     if (wave == 0) {
-        uint32_t w = lane < kPBlock / 64 ? wsum[lane] : 0;
+        const uint32_t w = lane < kPBlock / 64 ? wsum[lane] : 0;
         uint32_t wi = w;
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
             const uint32_t y = __shfl_up(wi, o);
             if (lane >= (uint32_t)o) wi += y;
         }
-        if (lane < kPBlock / 64) wsum[lane] = wi - w;  // exclusive wave offsets
+        if (lane < kPBlock / 64) wsum[lane] = wi - w;
     }
     __syncthreads();
     uint32_t run = wsum[wave] + incl - sum;
@@ -79,25 +91,26 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
     }
 }
 
-// KS = stash slots per lane: 32 -> one 1024-thread workgroup per CU (big tiles, long runs);
-// 16 -> two per CU (8 waves/SIMD for the hashing, shorter runs).
-template <int FMT, bool LP, int KS>
-__global__ __launch_bounds__(kPBlock, KS == 16 ? 8 : 4) void k_tile_sort(DevKeys dk, PartPlan pl,
-                                                                         uint32_t* tiles, uint16_t* ends) {
+template <int FMT, bool LP>
+__global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, uint32_t* tiles,
+                                                       uint16_t* ends) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t* sorted = smem;            // C entries
-    uint32_t* cnt = smem + pl.C;        // nseg entries (+ pad)
-    uint32_t* wsum = cnt + ((pl.nseg + 3) & ~3u);
+    uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // CP entries
+    uint32_t* hi = smem + pl.CP / 2;                    // CP/8 words, 8 nibbles each
+    uint32_t* cnt = hi + pl.CP / 8;                     // nseg_pad
+    uint32_t* wsum = cnt + pl.nseg_pad;                 // 16
     const uint32_t tid = threadIdx.x;
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
+    for (uint32_t w = tid; w < pl.CP / 8; w += kPBlock) hi[w] = 0;
     __syncthreads();
 
-    uint32_t stash[KS];
+    uint32_t stash[kStash];
     uint32_t ns = 0;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
+    const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
     for (uint32_t r = 0; r < pl.R; ++r) {
         const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
-        const bool valid = j < dk.n;
+        const bool valid = j < key_end;
         Prefix p{};
         if (valid) p = key_prefix<FMT, LP>(dk, j);
         for (uint32_t i = 0; i < pl.k; ++i) {
@@ -109,6 +122,8 @@ __global__ __launch_bounds__(kPBlock, KS == 16 ? 8 : 4) void k_tile_sort(DevKeys
             stash[ns++] = idx;
         }
     }
+    __syncthreads();
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = (cnt[s] + 1) & ~1u;  // even runs
     __syncthreads();
     block_exclusive_scan(cnt, pl.nseg, wsum);
     __syncthreads();
@@ -121,70 +136,39 @@ __global__ __launch_bounds__(kPBlock, KS == 16 ? 8 : 4) void k_tile_sort(DevKeys
             pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> kSegBits], 1u) : 0u;
         }
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (val[q] != kSentinel) sorted[pos[q]] = val[q];
-    }
-    __syncthreads();
-    // cnt[s] now holds the end of segment s's run within the sorted tile
-    const uint32_t total = cnt[pl.nseg - 1];
-    uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.C;
-    const uint32_t total4 = total & ~3u;
-    for (uint32_t e = tid * 4; e < total4; e += kPBlock * 4)
-        *reinterpret_cast<uint4*>(out + e) = *reinterpret_cast<const uint4*>(sorted + e);
-    for (uint32_t e = total4 + tid; e < total; e += kPBlock) out[e] = sorted[e];
-    uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nseg;
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)cnt[s];
-}
-
-// Same tile contract, no LDS copy of the tile: each index is stored straight to its sorted slot
-// in the tile's global region (the block's 120 KiB of scattered 4-byte stores land in L2 within
-// a few microseconds and leave as whole lines).  LDS holds only the counters, so two
-// 1024-thread workgroups fit per CU (8 waves/SIMD for the hashing).
-template <int FMT, bool LP>
-__global__ __launch_bounds__(kPBlock) void k_tile_sort_direct(DevKeys dk, PartPlan pl, uint32_t* tiles,
-                                                                 uint16_t* ends) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t* cnt = smem;  // nseg entries (+ pad)
-    uint32_t* wsum = cnt + ((pl.nseg + 3) & ~3u);
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
-    __syncthreads();
-
-    uint32_t stash[kStash];
-    uint32_t ns = 0;
-    const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
-    for (uint32_t r = 0; r < pl.R; ++r) {
-        const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
-        const bool valid = j < dk.n;
-        Prefix p{};
-        if (valid) p = key_prefix<FMT, LP>(dk, j);
-        for (uint32_t i = 0; i < pl.k; ++i) {
-            uint32_t idx = kSentinel;
-            if (valid) {
-                idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
-                atomicAdd(&cnt[idx >> kSegBits], 1u);
-            }
-            stash[ns++] = idx;
-        }
-    }
-    __syncthreads();
-    block_exclusive_scan(cnt, pl.nseg, wsum);
-    __syncthreads();
-    uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.C;
-    for (uint32_t t = 0; t < ns; t += 8) {
-        uint32_t pos[8], val[8];
-#pragma unroll
         for (int q = 0; q < 8; ++q) {
-            val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> kSegBits], 1u) : 0u;
+            if (val[q] != kSentinel) {
+                lo[pos[q]] = (uint16_t)val[q];
+                atomicOr(&hi[pos[q] >> 3], ((val[q] >> 16) & 15u) << ((pos[q] & 7) * 4));
+            }
         }
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (val[q] != kSentinel) out[pos[q]] = val[q];
     }
     __syncthreads();
+    // cnt[s] = start(s) + count(s) with every start even: an odd cnt marks an odd run, padded
+    // with a copy of its last index.
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) {
+        const uint32_t c = cnt[s];
+        if (c & 1u) {
+            lo[c] = lo[c - 1];
+            const uint32_t nib = (hi[(c - 1) >> 3] >> (((c - 1) & 7) * 4)) & 15u;
+            atomicOr(&hi[c >> 3], nib << ((c & 7) * 4));
+        }
+    }
+    __syncthreads();
+    const uint32_t total = (cnt[pl.nseg - 1] + 1) & ~1u;
+    uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.tile_words;
+    const uint32_t lo_words = total / 2;
+    for (uint32_t w = tid * 4; w < lo_words; w += kPBlock * 4) {
+        if (w + 4 <= lo_words)
+            *reinterpret_cast<uint4*>(out + w) = *reinterpret_cast<const uint4*>(smem + w);
+        else
+            for (uint32_t x = w; x < lo_words; ++x) out[x] = smem[x];
+    }
+    uint32_t* out_hi = out + pl.CP / 2;
+    const uint32_t hi_words = (total + 7) / 8;
+    for (uint32_t w = tid; w < hi_words; w += kPBlock) out_hi[w] = hi[w];
     uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nseg;
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)cnt[s];
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)((cnt[s] + 1) & ~1u);
 }
 
 // ends[rows][cols] -> endsT[cols][rows], 64x64 tiles through LDS.
@@ -204,12 +188,29 @@ __global__ __launch_bounds__(256) void k_transpose_u16(const uint16_t* in, uint1
     }
 }
 
-// Runs are read by 8-lane groups: lane q of a group loads words [4q, 4q+4) and [32+4q, 32+4q+4)
-// of its run with 16-byte loads (4-byte aligned: gfx950 global loads need only dword alignment),
-// so one wave instruction covers 8 runs x 128 contiguous bytes.  All 16 loads of the 64 runs a
-// wave owns are issued before the first ds_or; the few runs longer than 64 words finish in a
-// tail loop.  Words past a run's end belong to the next run of the same tile (or to the
-// workspace's tail pad) and are masked off.
+// OR 8 packed indices (8 u16 low halves + their 8 nibbles) into the segment bitmap.
+__device__ __forceinline__ void or8(uint32_t* bitmap, uint4 l, uint32_t nib, uint32_t valid) {
+    const uint32_t w[4] = {l.x, l.y, l.z, l.w};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        if ((uint32_t)c < valid) {
+            const uint32_t idx = ((w[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) | (((nib >> (4 * c)) & 15u) << 16);
+            atomicOr(&bitmap[idx >> 5], 1u << (idx & 31));
+        }
+    }
+}
+
+// Loads elements [e, e+8) of a packed tile: 16 bytes of low halves (e even -> dword aligned) and
+// the 8 nibbles from the two nibble words around e.  Bytes past the run belong to the same tile
+// or to the workspace's tail pad and are masked by the caller.
+__device__ __forceinline__ void load8(const uint32_t* tile, uint32_t cp, uint32_t e, uint4& l, uint32_t& nib) {
+    __builtin_memcpy(&l, tile + e / 2, 16);
+    uint2 h;
+    __builtin_memcpy(&h, tile + cp / 2 + (e >> 3), 8);
+    const uint64_t hh = ((uint64_t)h.y << 32) | h.x;
+    nib = (uint32_t)(hh >> ((e & 7) * 4));
+}
+
 __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const uint16_t* endsT,
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
                                                     uint32_t* words) {
@@ -238,48 +239,40 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / pl.G);
     const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
     const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * ntiles : nullptr;
-    const uint32_t grp = lane >> 3, q4 = (lane & 7) * 4;
+    const uint32_t grp = lane >> 3, q8 = (lane & 7) * 8;
     for (uint32_t tg = t_lo + wave * 64; tg < t_hi; tg += kPBlock) {
-        // element offsets fit u32: one chunk holds < 2^30 + C indices (kPartChunkIdx)
-        uint32_t off[8], len[8];
-        uint4 d0[8], d1[8];
+        uint32_t st[8], len[8], nib[8];
+        uint4 l[8];
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             const uint32_t t = tg + g * 8 + grp;  // the 8 lanes of a group read the same u16
-            uint32_t st = 0, en = 0;
+            uint32_t b = 0, e = 0;
             if (t < t_hi) {
-                st = row_beg ? row_beg[t] : 0;
-                en = row_end[t];
+                b = row_beg ? row_beg[t] : 0;
+                e = row_end[t];
             }
-            off[g] = t * pl.C + st + q4;
-            len[g] = en - st;
+            st[g] = b;
+            len[g] = e - b;
         }
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            if (q4 < len[g]) __builtin_memcpy(&d0[g], tiles + off[g], 16);
-            if (q4 + 32 < len[g]) __builtin_memcpy(&d1[g], tiles + off[g] + 32, 16);
+            if (q8 < len[g]) {
+                const uint32_t* tile = tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words;
+                load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
+            }
         }
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const uint32_t a[4] = {d0[g].x, d0[g].y, d0[g].z, d0[g].w};
-            const uint32_t b[4] = {d1[g].x, d1[g].y, d1[g].z, d1[g].w};
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (q4 + c < len[g]) atomicOr(&bitmap[(a[c] >> 5) & (kSegWords - 1)], 1u << (a[c] & 31));
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (q4 + 32 + c < len[g]) atomicOr(&bitmap[(b[c] >> 5) & (kSegWords - 1)], 1u << (b[c] & 31));
-        }
-        // tail: runs longer than 64 words (rare at the default plan; common for tiny m)
+        for (int g = 0; g < 8; ++g)
+            if (q8 < len[g]) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len[g] - q8));
+        // tail: runs longer than 64 indices (rare at the default plan; common for tiny m)
 #pragma unroll 1
         for (int g = 0; g < 8; ++g) {
-            for (uint32_t e = q4 + 64; e < len[g]; e += 32) {
-                uint4 v;
-                __builtin_memcpy(&v, tiles + off[g] - q4 + e, 16);
-                const uint32_t x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    if (e + c < len[g]) atomicOr(&bitmap[(x[c] >> 5) & (kSegWords - 1)], 1u << (x[c] & 31));
+            const uint32_t* tile = tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words;
+            for (uint32_t e = q8 + 64; e < len[g]; e += 64) {
+                uint4 lt;
+                uint32_t nt;
+                load8(tile, pl.CP, st[g] + e, lt, nt);
+                or8(bitmap, lt, nt, std::min<uint32_t>(8, len[g] - e));
             }
         }
     }
@@ -299,46 +292,53 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     }
 }
 
-static int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
-static uint32_t stash_slots(uint32_t k) {
-    static const int env = env_int("VBF_TILE_KS", 0);
-    if (env == 16 && k <= 16) return 16;
-    return 32;
-}
-
-// K1 variant: 0 = LDS-sorted tile copy, 1 = direct scattered stores (VBF_TILE_DIRECT)
-static int tile_direct() {
-    static const int env = env_int("VBF_TILE_DIRECT", 0);
-    return env;
-}
-
+// Tile size: the largest KT (<= kStash/k rounds of 1024 keys) whose packed LDS image fits two
+// workgroups per CU; one per CU only when two cannot hold a single round of keys.
 static PartPlan make_plan(uint32_t m, uint32_t k) {
     PartPlan pl{};
     pl.k = k;
-    pl.KS = stash_slots(k);
-    pl.R = pl.KS / k;
-    pl.KT = pl.R * kPBlock;
-    pl.C = pl.KT * k;
     pl.m = m;
     pl.mu = ~0ull / m;
     pl.nwords = ((uint64_t)m + 31) / 32;
     pl.nseg = (uint32_t)(((uint64_t)m + (1u << kSegBits) - 1) >> kSegBits);
+    pl.nseg_pad = (pl.nseg + 3) & ~3u;
+    const uint32_t rmax = kStash / k;
+    for (uint32_t per_cu : {2u, 1u}) {
+        const uint32_t budget = kLdsPerCu / per_cu;
+        const int64_t avail = (int64_t)budget - 64 - 4 * (int64_t)pl.nseg_pad;
+        // LDS = 2.5 * CP with CP <= C + nseg + 8
+        const int64_t cmax = avail * 2 / 5 - pl.nseg - 8;
+        const int64_t kt = std::min<int64_t>((int64_t)rmax * kPBlock, cmax / k);
+        if (kt >= kPBlock || per_cu == 1) {
+            pl.KT = (uint32_t)std::max<int64_t>(kt, 1);
+            break;
+        }
+    }
+    pl.R = (pl.KT + kPBlock - 1) / kPBlock;
+    pl.C = pl.KT * k;
+    pl.CP = (pl.C + pl.nseg + 7) & ~7u;
+    pl.tile_words = pl.CP / 2 + pl.CP / 8;
+    pl.lds1 = (pl.CP / 2 + pl.CP / 8 + pl.nseg_pad + 16) * 4;
     return pl;
 }
 
-bool partition_supported(uint32_t m, uint32_t k) { return m > 0 && k >= 1 && k <= (uint32_t)kStash; }
+bool partition_supported(uint32_t m, uint32_t k) {
+    if (m == 0 || k < 1 || k > (uint32_t)kStash) return false;
+    const PartPlan pl = make_plan(m, k);
+    return pl.lds1 <= kLdsPerCu && pl.CP <= 65535;
+}
+
+static uint64_t chunk_keys_for(const PartPlan& pl, uint64_t n) {
+    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, kPartChunkIdx / pl.C);
+    return std::min<uint64_t>(n, tiles_per_chunk * pl.KT);
+}
 
 // Bytes of workspace one launch_build_partitioned call needs for n keys.
 uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     if (!partition_supported(m, k)) return 0;
     const PartPlan pl = make_plan(m, k);
-    uint64_t chunk_keys = std::min<uint64_t>(n, kPartChunkIdx / k);
-    const uint64_t ntiles = (chunk_keys + pl.KT - 1) / pl.KT;
-    return ntiles * ((uint64_t)pl.C * 4 + (uint64_t)pl.nseg * 4) + 512;
+    const uint64_t ntiles = (chunk_keys_for(pl, n) + pl.KT - 1) / pl.KT;
+    return ntiles * ((uint64_t)pl.tile_words * 4 + (uint64_t)pl.nseg * 4) + 512;
 }
 
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
@@ -346,15 +346,13 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
     if (kb.n == 0 || k == 0) return hipSuccess;
     if (!partition_supported(m, k)) return hipErrorInvalidValue;
     PartPlan pl = make_plan(m, k);
-    const uint64_t chunk_keys = std::min<uint64_t>(kb.n, (kPartChunkIdx / k) / pl.KT * pl.KT);
+    const uint64_t chunk_keys = chunk_keys_for(pl, kb.n);
     const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
     if (ws_bytes < partition_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;
     uint32_t* tiles = reinterpret_cast<uint32_t*>(ws);
-    uint16_t* ends = reinterpret_cast<uint16_t*>(tiles + max_tiles * pl.C);
+    uint16_t* ends = reinterpret_cast<uint16_t*>(tiles + max_tiles * pl.tile_words);
     uint16_t* endsT = ends + max_tiles * pl.nseg;
 
-    const bool direct = tile_direct() && pl.KS == 32;
-    const size_t lds1 = ((size_t)(direct ? 0 : pl.C) + ((pl.nseg + 3) & ~3u) + 64) * 4;
     for (uint64_t lo = 0; lo < kb.n; lo += chunk_keys) {
         const uint64_t cn = std::min<uint64_t>(chunk_keys, kb.n - lo);
         DevKeys dk{kb.keys, kb.offsets, kb.off_base, kb.stride, cn};
@@ -366,12 +364,11 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         hipError_t err = hipSuccess;
         phase_begin(kPhaseTileSort, s);
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
-            auto fn = direct ? k_tile_sort_direct<FMT, LP>
-                             : pl.KS == 16 ? k_tile_sort<FMT, LP, 16> : k_tile_sort<FMT, LP, 32>;
+            auto fn = k_tile_pack<FMT, LP>;
             err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1);
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
             if (err == hipSuccess)
-                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), lds1, s, dk, pl, tiles, ends);
+                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
         });
         if (err != hipSuccess) return err;
         phase_end(kPhaseTileSort, s);
