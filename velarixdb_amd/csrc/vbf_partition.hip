@@ -215,7 +215,12 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
                                                     uint32_t* words) {
     __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
-    const uint32_t seg = blockIdx.x / pl.G, part = blockIdx.x % pl.G;
+    // XCD-aware order (blocks are dealt round-robin over the 8 XCDs; speed only, never
+    // correctness): consecutive segments run on one XCD at the same time, and since a tile
+    // stores its segments' runs back to back, they share the L2 lines those short runs sit in.
+    const uint32_t nwg = gridDim.x, q = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+    const uint32_t wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + blockIdx.x / 8;
+    const uint32_t seg = wg / pl.G, part = wg % pl.G;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t wbase = (uint64_t)seg * kSegWords;
     const uint32_t wn = (uint32_t)std::min<uint64_t>(kSegWords, pl.nwords - wbase);
