@@ -40,6 +40,10 @@ constexpr uint32_t kSegWords = 1u << (kSegBits - 5);
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a bit index: idx < m <= 2^32 - 1
 constexpr uint32_t kLdsPerCu = 163840;
 
+// Rounds of 1024 keys a lane can stash: kStash / k indices, but k = 4 keeps 24 so the fully
+// unrolled K = 4 kernel stays within 64 VGPRs (two workgroups per CU) without spilling.
+__host__ __device__ constexpr int rounds_max(int k) { return k == 4 ? 6 : kStash / k; }
+
 struct PartPlan {
     uint32_t k;
     uint32_t R;           // hashing rounds per lane (ceil(KT / 1024))
@@ -91,7 +95,9 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
     }
 }
 
-template <int FMT, bool LP>
+// K > 0: k known at compile time (the stash and seed loops unroll, no indexed register moves);
+// K == 0: any k <= kStash at run time.
+template <int FMT, bool LP, int K>
 __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, uint32_t* tiles,
                                                        uint16_t* ends) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -105,21 +111,43 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     __syncthreads();
 
     uint32_t stash[kStash];
-    uint32_t ns = 0;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
     const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
-    for (uint32_t r = 0; r < pl.R; ++r) {
-        const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
-        const bool valid = j < key_end;
-        Prefix p{};
-        if (valid) p = key_prefix<FMT, LP>(dk, j);
-        for (uint32_t i = 0; i < pl.k; ++i) {
-            uint32_t idx = kSentinel;
-            if (valid) {
-                idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
-                atomicAdd(&cnt[idx >> kSegBits], 1u);
+    uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
+    if constexpr (K > 0) {
+        constexpr int RM = rounds_max(K);
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+            const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
+            const bool valid = (uint32_t)r < pl.R && j < key_end;
+            Prefix p{};
+            if (valid) p = key_prefix<FMT, LP>(dk, j);
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                uint32_t idx = kSentinel;
+                if (valid) {
+                    idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
+                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                }
+                stash[r * K + i] = idx;
             }
-            stash[ns++] = idx;
+        }
+        ns = RM * K;
+    } else {
+        ns = 0;
+        for (uint32_t r = 0; r < pl.R; ++r) {
+            const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
+            const bool valid = j < key_end;
+            Prefix p{};
+            if (valid) p = key_prefix<FMT, LP>(dk, j);
+            for (uint32_t i = 0; i < pl.k; ++i) {
+                uint32_t idx = kSentinel;
+                if (valid) {
+                    idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
+                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                }
+                stash[ns++] = idx;
+            }
         }
     }
     __syncthreads();
@@ -128,6 +156,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     block_exclusive_scan(cnt, pl.nseg, wsum);
     __syncthreads();
     // rank + place, 8 returning LDS atomics in flight before their results are used
+#pragma unroll
     for (uint32_t t = 0; t < ns; t += 8) {
         uint32_t pos[8], val[8];
 #pragma unroll
@@ -245,9 +274,9 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
     const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * ntiles : nullptr;
     const uint32_t grp = lane >> 3, q8 = (lane & 7) * 8;
-    for (uint32_t tg = t_lo + wave * 64; tg < t_hi; tg += kPBlock) {
-        uint32_t st[8], len[8], nib[8];
-        uint4 l[8];
+    // Two-stage pipeline over the wave's 64-tile batches: the run bounds of batch b+1 and the
+    // data of batch b are in flight together, so each batch costs one memory latency, not two.
+    auto bounds = [&](uint32_t tg, uint32_t (&st)[8], uint32_t (&len)[8]) {
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             const uint32_t t = tg + g * 8 + grp;  // the 8 lanes of a group read the same u16
@@ -259,6 +288,14 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
             st[g] = b;
             len[g] = e - b;
         }
+    };
+    const uint32_t step = kPBlock;  // 16 waves x 64 tiles
+    uint32_t tg = t_lo + wave * 64;
+    uint32_t st[8], len[8];
+    bounds(tg, st, len);
+    while (tg < t_hi) {
+        uint32_t nib[8];
+        uint4 l[8];
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
             if (q8 < len[g]) {
@@ -266,6 +303,9 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
                 load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
             }
         }
+        const uint32_t tn = tg + step;
+        uint32_t st2[8], len2[8];
+        bounds(tn, st2, len2);
 #pragma unroll
         for (int g = 0; g < 8; ++g)
             if (q8 < len[g]) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len[g] - q8));
@@ -280,6 +320,12 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
                 or8(bitmap, lt, nt, std::min<uint32_t>(8, len[g] - e));
             }
         }
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {
+            st[g] = st2[g];
+            len[g] = len2[g];
+        }
+        tg = tn;
     }
     __syncthreads();
     if (own) {
@@ -307,7 +353,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.nwords = ((uint64_t)m + 31) / 32;
     pl.nseg = (uint32_t)(((uint64_t)m + (1u << kSegBits) - 1) >> kSegBits);
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
-    const uint32_t rmax = kStash / k;
+    const uint32_t rmax = (uint32_t)rounds_max((int)k);
     for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
         const int64_t avail = (int64_t)budget - 64 - 4 * (int64_t)pl.nseg_pad;
@@ -369,7 +415,11 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         hipError_t err = hipSuccess;
         phase_begin(kPhaseTileSort, s);
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
-            auto fn = k_tile_pack<FMT, LP>;
+            auto fn = k == 10 ? k_tile_pack<FMT, LP, 10>
+                    : k == 4  ? k_tile_pack<FMT, LP, 4>
+                    : k == 19 ? k_tile_pack<FMT, LP, 19>
+                    : k == 9  ? k_tile_pack<FMT, LP, 9>
+                              : k_tile_pack<FMT, LP, 0>;
             err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
             if (err == hipSuccess)
