@@ -163,6 +163,28 @@ __global__ __launch_bounds__(256) void k_gather(const uint32_t* w, uint32_t nw, 
     if (acc == 0xdeadbeef) out[0] = acc;
 }
 
+// LDS op throughput: every lane issues N ops at pseudo-random word addresses of a 32K-word
+// (128 KiB) LDS array.  OP: 0 ds_or (atomic, no return), 1 ds_add_rtn, 2 ds_write_b32,
+// 3 ds_write_b16, 4 ds_or with value 0 on odd lanes (branch-free masking).
+template <int OP>
+__global__ __launch_bounds__(1024) void k_lds(int n, uint32_t* out) {
+    __shared__ uint32_t a[32768];
+    for (int i = threadIdx.x; i < 32768; i += 1024) a[i] = 0;
+    __syncthreads();
+    uint32_t x = (blockIdx.x * 1024 + threadIdx.x) * 2654435761u + 1, acc = 0;
+    for (int i = 0; i < n; ++i) {
+        x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+        const uint32_t w = x & 32767;
+        if constexpr (OP == 0) atomicOr(&a[w], 1u << (x >> 27));
+        else if constexpr (OP == 1) acc += atomicAdd(&a[w], 1u);
+        else if constexpr (OP == 2) a[w] = x;
+        else if constexpr (OP == 3) reinterpret_cast<uint16_t*>(a)[x & 65535] = (uint16_t)x;
+        else atomicOr(&a[w], (threadIdx.x & 1) ? 0u : (1u << (x >> 27)));
+    }
+    __syncthreads();
+    if (acc == 0xdeadbeef || a[threadIdx.x] == 0xdeadbeef) out[0] = acc;
+}
+
 template <class F>
 static float time_ms(F&& f, int reps) {
     hipEvent_t a, b;
@@ -203,6 +225,23 @@ int main() {
         run(k_hash2<1, 1024>, 1024, 120 * 1024, "V1 + mod, 1024 thr, 1 block/CU (LDS)");
         run(k_hash2<2, 1024>, 1024, 120 * 1024, "V1 2-seed + mod, 1024 thr, 1 block/CU");
         run(k_hash2<3, 1024>, 1024, 120 * 1024, "V3 addc + mod, 1024 thr, 1 block/CU");
+    }
+    {
+        uint32_t* o;
+        CHECK(hipMalloc(&o, 4));
+        const int nops = 4096, blocks = 256 * 4;
+        auto run = [&](auto kern, const char* name) {
+            float t = time_ms([&] { hipLaunchKernelGGL(kern, dim3(blocks), dim3(1024), 0, 0, nops, o); }, 3);
+            const double ops = (double)blocks * 1024 * nops;
+            printf("  LDS %-28s %.3f ms  %.1f G lane-ops/s  (%.1f lane-ops/clk/CU at 2.2 GHz)\n", name, t,
+                   ops / t / 1e6, ops / (t * 1e-3) / 256 / 2.2e9);
+        };
+        printf("LDS random-address throughput (1024-thread blocks, 1 per CU at a time):\n");
+        run(k_lds<0>, "ds_or_b32 (atomic)");
+        run(k_lds<1>, "ds_add_rtn_u32");
+        run(k_lds<2>, "ds_write_b32");
+        run(k_lds<3>, "ds_write_b16");
+        run(k_lds<4>, "ds_or_b32, half lanes or 0");
     }
     uint32_t* w;
     const uint64_t maxw = 1ull << 29;  // 2 GiB
