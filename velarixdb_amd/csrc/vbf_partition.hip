@@ -217,15 +217,15 @@ __global__ __launch_bounds__(256) void k_transpose_u16(const uint16_t* in, uint1
     }
 }
 
-// OR 8 packed indices (8 u16 low halves + their 8 nibbles) into the segment bitmap.  Branch-free:
-// entries at or past `valid` OR a zero (a no-op) into whatever word their garbage names.
+// OR 8 packed indices (8 u16 low halves + their 8 nibbles) into the segment bitmap.
 __device__ __forceinline__ void or8(uint32_t* bitmap, uint4 l, uint32_t nib, uint32_t valid) {
     const uint32_t w[4] = {l.x, l.y, l.z, l.w};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        const uint32_t idx = ((w[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) | (((nib >> (4 * c)) & 15u) << 16);
-        const uint32_t bit = (uint32_t)c < valid ? (1u << (idx & 31)) : 0u;
-        atomicOr(&bitmap[idx >> 5], bit);
+        if ((uint32_t)c < valid) {
+            const uint32_t idx = ((w[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) | (((nib >> (4 * c)) & 15u) << 16);
+            atomicOr(&bitmap[idx >> 5], 1u << (idx & 31));
+        }
     }
 }
 
@@ -296,19 +296,19 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     while (tg < t_hi) {
         uint32_t nib[8];
         uint4 l[8];
-        // every lane loads (tile index clamped into range): no branches around the loads
 #pragma unroll
         for (int g = 0; g < 8; ++g) {
-            const uint32_t t = std::min(tg + g * 8 + grp, t_hi - 1);
-            const uint32_t* tile = tiles + (uint64_t)t * pl.tile_words;
-            load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
+            if (q8 < len[g]) {
+                const uint32_t* tile = tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words;
+                load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
+            }
         }
         const uint32_t tn = tg + step;
         uint32_t st2[8], len2[8];
         bounds(tn, st2, len2);
 #pragma unroll
         for (int g = 0; g < 8; ++g)
-            or8(bitmap, l[g], nib[g], len[g] > q8 ? std::min<uint32_t>(8, len[g] - q8) : 0u);
+            if (q8 < len[g]) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len[g] - q8));
         // tail: runs longer than 64 indices (rare at the default plan; common for tiny m)
 #pragma unroll 1
         for (int g = 0; g < 8; ++g) {
