@@ -31,6 +31,20 @@ from velarixdb_amd import workloads as wl  # noqa: E402
 from velarixdb_amd._lib import call  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32 lane-ops/s)
+# VALU lane-instructions per key of the build, from rocprofv3 SQ_INSTS_VALU (profiles/r01)
+VALU_PER_KEY_CFG2 = 1706.0
+
+
+def pmc_traffic(name):
+    """Per-launch HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes."""
+    path = os.path.join(ROOT, "profiles", "r01", name)
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["per_launch_bytes"], "profiles/r01/" + name
+    except (OSError, ValueError, KeyError):
+        return None, None
 
 
 def vp(t):
@@ -152,6 +166,8 @@ def bench_fixed(ctx, args):
     kavg = float(np.mean(kms)) / 1e3
     bytes_per_key = L + m / (8.0 * n)
     achieved = n * bytes_per_key / kavg / 1e9
+    traffic, traffic_src = (pmc_traffic("traffic_config2.json") if (n, L, k) == (100_000_000, 16, 10)
+                            and args.strategy != 1 else (None, None))
     res = {
         "metric": "Bloom build keys/s (device-resident keys, bit-exact SipHash-1-3 filter)",
         "value": value, "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps,
@@ -164,8 +180,9 @@ def bench_fixed(ctx, args):
             "n_keys_per_gpu": n, "key_bytes": L, "m_bits": m, "k": k, "len_prefix": True,
             "parallelism": "independent shards x%d" % ctx.world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "build (all phases of one vbf_build_dev_ex launch)", "kernel_ms": kavg * 1e3,
+                     "valu_frac_est": n * VALU_PER_KEY_CFG2 / kavg / VALU_PEAK_LANE_OPS,
                      "algorithmic_bytes_per_key": bytes_per_key,
                      "siprounds_per_key": (L + 8) // 8 + 5 * k,
                      "phases": phase_report(phases, args.steps)},
