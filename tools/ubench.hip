@@ -50,6 +50,16 @@ __device__ __forceinline__ uint64_t add_nv(uint64_t a, uint64_t b) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// swap32(a) + b with explicit 32-bit carry ops: the halves of a are consumed crosswise, so no
+// register-pair re-alignment is needed (V5).
+__device__ __forceinline__ uint64_t add_sw(uint64_t a, uint64_t b) {
+    unsigned c0, c1;
+    const unsigned lo = __builtin_addc((unsigned)(a >> 32), (unsigned)b, 0u, &c0);
+    const unsigned hi = __builtin_addc((unsigned)a, (unsigned)(b >> 32), c0, &c1);
+    (void)c1;
+    return ((uint64_t)hi << 32) | lo;
+}
+
 template <int V>
 __device__ __forceinline__ void round_(S& s) {
     if constexpr (V == 0) {
@@ -62,6 +72,13 @@ __device__ __forceinline__ void round_(S& s) {
         s.v2 += s.v3; s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
         s.v0 += s.v3; s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
         s.v2 += s.v1; s.v1 = rotl_a<17>(s.v1); s.v1 ^= s.v2; s.v2 = swap32(s.v2);
+    } else if constexpr (V == 5) {
+        // v0, v2 are kept UNswapped where a swap would feed an add: add_sw folds the swap in
+        s.v0 += s.v1; s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0;
+        s.v2 = add_sw(s.v2, s.v3); s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
+        s.v0 = add_sw(s.v0, s.v3); s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
+        s.v2 += s.v1; s.v1 = rotl_a<17>(s.v1); s.v1 ^= s.v2;
+        // at exit v2 is logically swap32(v2): the next round's first v2 use is add_sw (swap folded)
     } else if constexpr (V == 3) {
         s.v0 = add_nv(s.v0, s.v1); s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap32(s.v0);
         s.v2 = add_nv(s.v2, s.v3); s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
@@ -78,8 +95,17 @@ __device__ __forceinline__ void round_(S& s) {
 template <int V>
 __device__ __forceinline__ void comp(S& s, uint64_t m) { s.v3 ^= m; round_<V>(s); s.v0 ^= m; }
 
+// V5 representation: v2 is stored un-swapped between rounds (logical v2 = swap32(stored)).
+__device__ __forceinline__ uint64_t lv2(const S& s) { return swap32(s.v2); }
+
 template <int V>
 __device__ __forceinline__ uint64_t fin(S s, uint64_t b) {
+    if constexpr (V == 5) {
+        s.v3 ^= b; round_<5>(s); s.v0 ^= b;
+        s.v2 ^= (0xffull << 32);  // logical v2 ^= 0xff on the stored (swapped) form
+        round_<5>(s); round_<5>(s); round_<5>(s);
+        return s.v0 ^ s.v1 ^ lv2(s) ^ s.v3;
+    }
     s.v3 ^= b; round_<V>(s); s.v0 ^= b; s.v2 ^= 0xff; round_<V>(s); round_<V>(s); round_<V>(s);
     return s.v0 ^ s.v1 ^ s.v2 ^ s.v3;
 }
@@ -106,14 +132,16 @@ __device__ __forceinline__ uint32_t fmod_(uint64_t x, uint64_t m, uint64_t mu) {
     return (uint32_t)r;
 }
 
-// MODE: 0 = V1 hash only; 1 = V1 + mod; 2 = V1, two seeds interleaved, + mod; 3 = V3 + mod
+// MODE: 0 = V1 hash only; 1 = V1 + mod; 2 = V1, two seeds interleaved, + mod; 3 = V3 + mod;
+// 5 = V5 (swap folded into carry adds) + mod
 template <int MODE, int BS>
 __global__ __launch_bounds__(BS) void k_hash2(uint64_t n, int k, uint64_t m, uint64_t mu, uint64_t* out) {
     extern __shared__ uint32_t pad[];
     uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
     if (j >= n) return;
-    constexpr int V = MODE == 3 ? 3 : 1;
+    constexpr int V = MODE == 3 ? 3 : MODE == 5 ? 5 : 1;
     S s{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL, 0x7465646279746573ULL};
+    if constexpr (V == 5) s.v2 = swap32(s.v2);  // stored form
     comp<V>(s, 16); comp<V>(s, j * 0x9E3779B97F4A7C15ULL); comp<V>(s, j);
     uint64_t acc = 0;
     if constexpr (MODE == 2) {
@@ -199,11 +227,31 @@ static float time_ms(F&& f, int reps) {
     return ms / reps;
 }
 
+template <int V>
+__global__ void k_hash_check(uint64_t* out) {
+    const uint64_t j = threadIdx.x;
+    S s{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL, 0x7465646279746573ULL};
+    if constexpr (V == 5) s.v2 = swap32(s.v2);
+    comp<V>(s, 16); comp<V>(s, j * 0x9E3779B97F4A7C15ULL); comp<V>(s, j);
+    out[j] = fin<V>(s, 32ull << 56);
+}
+
 int main() {
     const uint64_t n = 100000000;
     uint64_t* out;
     CHECK(hipMalloc(&out, 8));
     const unsigned blocks = (unsigned)((n + 255) / 256);
+    {
+        uint64_t *c1, *c5;
+        CHECK(hipMalloc(&c1, 64 * 8)); CHECK(hipMalloc(&c5, 64 * 8));
+        hipLaunchKernelGGL(k_hash_check<1>, dim3(1), dim3(64), 0, 0, c1);
+        hipLaunchKernelGGL(k_hash_check<5>, dim3(1), dim3(64), 0, 0, c5);
+        uint64_t h1[64], h5[64];
+        CHECK(hipMemcpy(h1, c1, 512, hipMemcpyDeviceToHost)); CHECK(hipMemcpy(h5, c5, 512, hipMemcpyDeviceToHost));
+        int bad = 0;
+        for (int i = 0; i < 64; ++i) bad += h1[i] != h5[i];
+        printf("V5 == V1 hashes: %s\n", bad ? "MISMATCH" : "ok");
+    }
     float t0 = time_ms([&] { hipLaunchKernelGGL(k_hash<0>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
     float t1 = time_ms([&] { hipLaunchKernelGGL(k_hash<1>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
     float t2 = time_ms([&] { hipLaunchKernelGGL(k_hash<2>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
@@ -222,6 +270,7 @@ int main() {
         run(k_hash2<1, 256>, 256, 0, "V1 + mod, 256 thr");
         run(k_hash2<2, 256>, 256, 0, "V1 2-seed interleave + mod, 256 thr");
         run(k_hash2<3, 256>, 256, 0, "V3 addc + mod, 256 thr");
+        run(k_hash2<5, 256>, 256, 0, "V5 swap-folded carry adds + mod, 256 thr");
         run(k_hash2<1, 1024>, 1024, 120 * 1024, "V1 + mod, 1024 thr, 1 block/CU (LDS)");
         run(k_hash2<2, 1024>, 1024, 120 * 1024, "V1 2-seed + mod, 1024 thr, 1 block/CU");
         run(k_hash2<3, 1024>, 1024, 120 * 1024, "V3 addc + mod, 1024 thr, 1 block/CU");
