@@ -27,6 +27,8 @@ for s in $STEPS; do
     pytest) run pytest_gpu 1200 python -m pytest tests -x -q -m gpu ;;
     bench)  run bench 600 python bench.py ;;
     benchq)  run bench_quick 300 python bench.py --no-cpu-baseline ;;
+    benchnostagger) run bench_nostagger 300 env VBF_STAGGER=0 python bench.py --no-cpu-baseline ;;
+    benchstagger14) run bench_stagger14 300 env VBF_STAGGER=14 python bench.py --no-cpu-baseline ;;
     benchatomic) run bench_atomic 300 python bench.py --no-cpu-baseline --strategy 1 --steps 3 ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
     bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;

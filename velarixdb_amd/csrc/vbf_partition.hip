@@ -53,6 +53,7 @@ struct PartPlan {
     uint32_t nseg, nseg_pad, G;
     uint32_t tile_words;  // u32 words per tile in the workspace: CP/2 (lo16) + CP/8 (nibbles)
     uint32_t lds1;        // K1 dynamic LDS bytes
+    uint32_t stagger_lo, stagger_hi, stagger_sleeps;
     uint64_t m, mu, nwords;
 };
 
@@ -106,6 +107,12 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     uint32_t* cnt = hi + pl.CP / 8;                     // nseg_pad
     uint32_t* wsum = cnt + pl.nseg_pad;                 // 16
     const uint32_t tid = threadIdx.x;
+    // Stagger (speed only): the second workgroup dispatched to each CU starts ~half a tile
+    // later, so the two co-resident workgroups alternate hashing (VALU) and sorting (LDS)
+    // instead of contending for the same pipe at the same time.
+    if (blockIdx.x >= pl.stagger_lo && blockIdx.x < pl.stagger_hi) {
+        for (uint32_t i = 0; i < pl.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
     for (uint32_t w = tid; w < pl.CP / 8; w += kPBlock) hi[w] = 0;
     __syncthreads();
@@ -370,6 +377,13 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.CP = (pl.C + pl.nseg + 7) & ~7u;
     pl.tile_words = pl.CP / 2 + pl.CP / 8;
     pl.lds1 = (pl.CP / 2 + pl.CP / 8 + pl.nseg_pad + 16) * 4;
+    // stagger the second resident workgroup per CU by ~half a tile of hashing (~25 us at k=10,
+    // ~3000 keys): s_sleep 127 = 8128 cycles, ~3.7 us.  VBF_STAGGER=0 disables (A/B).
+    static const int env = [] { const char* e = getenv("VBF_STAGGER"); return e ? atoi(e) : -1; }();
+    const uint32_t sleeps = env >= 0 ? (uint32_t)env : 7;
+    pl.stagger_lo = 256;
+    pl.stagger_hi = 512;
+    pl.stagger_sleeps = sleeps;
     return pl;
 }
 
