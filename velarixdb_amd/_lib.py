@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvbf.so")
+# VBF_LIB selects an alternative in-tree build (A/B of compile-time variants); default libvbf.so
+LIB_PATH = os.environ.get("VBF_LIB") or os.path.join(_HERE, "libvbf.so")
 
 VBF_OK = 0
 VBF_EINVAL = -1

@@ -31,11 +31,15 @@
 #include "sip13.hpp"
 #include "vbf_kernels.hpp"
 
+#ifndef VBF_SEG_BITS
+#define VBF_SEG_BITS 20
+#endif
+
 namespace vbf {
 
 constexpr int kPBlock = 1024;                // threads per K1 / K3 workgroup
 constexpr int kStash = 32;                   // max bit indices a lane keeps in registers
-constexpr int kSegBits = 20;                 // segment = 2^20 bits = 128 KiB of LDS
+constexpr int kSegBits = VBF_SEG_BITS;       // segment = 2^20 bits = 128 KiB of LDS (default)
 constexpr uint32_t kSegWords = 1u << (kSegBits - 5);
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a bit index: idx < m <= 2^32 - 1
 constexpr uint32_t kLdsPerCu = 163840;
