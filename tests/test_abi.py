@@ -128,3 +128,23 @@ def test_product_never_imports_oracle():
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in txt and "liboracle" not in txt, f
                 assert "from oracle" not in txt, f
+
+
+def test_filter_file_extension_roundtrip():
+    """filter.db with persisted bits: the first 16 bytes stay the reference's format."""
+    import numpy as np
+    from velarixdb_amd import filter_file
+    w = np.arange(1, 1074, dtype=np.uint32) * np.uint32(2654435761)
+    raw = filter_file.encode(19, 1791, 1e-4, 34333, w)
+    assert raw[:16] == struct.pack("<IId", 19, 1791, 1e-4)
+    k, n, p, m, words = filter_file.decode(raw)
+    assert (k, n, p, m) == (19, 1791, 1e-4, 34333) and np.array_equal(words, w)
+    # corrupted body -> ignored (caller rebuilds, as the reference does)
+    bad = bytearray(raw)
+    bad[-1] ^= 0xFF
+    assert filter_file.decode(bytes(bad))[3:] == (None, None)
+    # the reference's own 16-byte files decode without words
+    ref = open(os.path.join(ROOT, "tests/golden/sst_fixtures/sstable_1720785462309/filter.db"), "rb").read()
+    assert filter_file.decode(ref) == (19, 1791, 1e-4, None, None)
+    with pytest.raises(EOFError):
+        filter_file.decode(ref[:12])

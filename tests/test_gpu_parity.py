@@ -344,3 +344,30 @@ def test_host_pointer_api_matches_device_api(vbf, ora):
     call("vbf_build_host", vdata.ctypes.data, off.ctypes.data, 0, nv, 1, m, k, w2.ctypes.data, w2.size, 0)
     from velarixdb_amd.keys import pack_offsets
     assert np.array_equal(w2, ora.build_words(pack_offsets(vdata, off), m, k, threads=8))
+
+
+def test_filter_db_persisted_bits(vbf, tmp_path):
+    """compaction-built filters (m from their own n) recover without a
+    rebuild and equal the rebuild; memtable-born ones (m from capacity) still need it."""
+    from velarixdb_amd import BloomFilter
+    keys = [b"k%06d" % i for i in range(17064)]
+    bf = BloomFilter(0.01, len(keys))  # compactors/sized.rs:192 sizing
+    bf.build_filter_from_entries(keys)
+    bf.write(tmp_path)
+    r = BloomFilter.default()
+    r.file_path = bf.file_path
+    assert r.recover_meta() is True
+    rebuilt = BloomFilter.default()
+    rebuilt.file_path = bf.file_path
+    assert rebuilt.recover_meta(load_bits=False) is False
+    rebuilt.build_filter_from_entries(keys)  # what range.rs:117-128 does
+    assert np.array_equal(r.words(), rebuilt.words())
+    # memtable-born: sized for 512 entries, holds 300 -> stored n = 300, m' != m
+    mem = BloomFilter(1e-4, 512)
+    mem.set_many(keys[:300])
+    d2 = tmp_path / "mem"
+    d2.mkdir()
+    mem.write(d2)
+    r2 = BloomFilter.default()
+    r2.file_path = mem.file_path
+    assert r2.recover_meta() is False and not r2.words().any()

@@ -24,7 +24,7 @@ import os
 
 import numpy as np
 
-from . import _lib
+from . import _lib, filter_file
 from ._lib import VBF_EDIVZERO, VBF_EINVAL, VbfError, call, lib
 from .keys import HostBatch, encode, pack
 
@@ -58,6 +58,7 @@ class BloomFilter:
     def __init__(self, false_positive_rate=None, no_of_elements=None, device=0, _handle=None):
         self.sst_dir = None
         self.file_path = None
+        self.bits_restored = False
         if _handle is not None:
             self._h = _handle
             return
@@ -205,33 +206,45 @@ class BloomFilter:
         call("vbf_filter_serialize", self._h, buf)
         return bytes(buf)
 
-    def write(self, dir_path):
-        """bf.rs:114-123: write `filter.db` (metadata only) and remember its path."""
+    def write(self, dir_path, persist_bits=True):
+        """bf.rs:114-123: write `filter.db` and remember its path.
+
+        The first 16 bytes are exactly the reference's.  With persist_bits the bit array follows
+        (filter_file.py): invisible to the reference's reader, used by recover_meta() here."""
         path = os.path.join(os.fspath(dir_path), FILTER_FILE_NAME + ".db")
+        m = self.num_bits()
+        words = self.words() if (persist_bits and m) else None
+        raw = filter_file.encode(self.no_of_hash_func, self.no_of_elements, self.false_positive_rate,
+                                 m, words)
+        assert raw[:16] == self.serialize()
         with open(path, "wb") as f:
-            f.write(self.serialize())
+            f.write(raw)
         self.file_path = path
 
-    def recover_meta(self):
-        """bf.rs:135-150: k and n from filter.db, m recomputed from n, zeroed bits."""
+    def recover_meta(self, load_bits=True):
+        """bf.rs:135-150: k and n from filter.db, m recomputed from n, zeroed bits.
+
+        Returns True when persisted bits were loaded (their m equals the recomputed m, so they
+        equal what the reference's rebuild from data.db produces and the rebuild can be
+        skipped); False when the caller must rebuild, as the reference always does."""
         if self.file_path is None:
             raise FileNotFoundError("File path for filter not provided (err/mod.rs:19-20)")
         try:
             with open(self.file_path, "rb") as f:
-                meta = f.read(16)
+                raw = f.read()
         except OSError:
             raise FileNotFoundError("Error opening filter file %s" % self.file_path) from None
-        buf = (ctypes.c_uint8 * max(len(meta), 1)).from_buffer_copy(meta.ljust(max(len(meta), 1), b"\0"))
+        k, n, p, m_saved, words = filter_file.decode(raw)
+        meta = (ctypes.c_uint8 * 16).from_buffer_copy(raw[:16])
         h = ctypes.c_void_p()
-        try:
-            call("vbf_filter_recover", buf, len(meta), self.device, ctypes.byref(h))
-        except VbfError as e:
-            if e.code == VBF_EINVAL:
-                raise EOFError("unexpected EOF reading %s" % self.file_path) from None
-            raise
+        call("vbf_filter_recover", meta, 16, self.device, ctypes.byref(h))
         old = self._h
         self._h = h
         lib.vbf_filter_free(old)
+        self.bits_restored = bool(load_bits and words is not None and m_saved == self.num_bits())
+        if self.bits_restored:
+            self.load_words(words)
+        return self.bits_restored
 
     def __repr__(self):
         return "BloomFilter(m=%d, k=%d, n=%d, p=%g, device=%d)" % (
