@@ -41,6 +41,8 @@ constexpr int kPBlock = 1024;                // threads per K1 / K3 workgroup
 constexpr int kStash = 32;                   // max bit indices a lane keeps in registers
 constexpr int kSegBits = VBF_SEG_BITS;       // segment = 2^20 bits = 128 KiB of LDS (default)
 constexpr uint32_t kSegWords = 1u << (kSegBits - 5);
+constexpr uint32_t kNibMask = (1u << (kSegBits - 16)) - 1;  // in-segment offset bits above 16
+static_assert(kSegBits > 16 && kSegBits <= 20, "offset = u16 + up to 4 nibble bits");
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a bit index: idx < m <= 2^32 - 1
 constexpr uint32_t kLdsPerCu = 163840;
 
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
         for (int q = 0; q < 8; ++q) {
             if (val[q] != kSentinel) {
                 lo[pos[q]] = (uint16_t)val[q];
-                atomicOr(&hi[pos[q] >> 3], ((val[q] >> 16) & 15u) << ((pos[q] & 7) * 4));
+                atomicOr(&hi[pos[q] >> 3], ((val[q] >> 16) & kNibMask) << ((pos[q] & 7) * 4));
             }
         }
     }
