@@ -29,8 +29,7 @@ for s in $STEPS; do
     benchq)  run bench_quick 300 python bench.py --no-cpu-baseline ;;
     benchnostagger) run bench_nostagger 300 env VBF_STAGGER=0 python bench.py --no-cpu-baseline ;;
     benchstagger14) run bench_stagger14 300 env VBF_STAGGER=14 python bench.py --no-cpu-baseline ;;
-    benchseg19) run bench_seg19 300 env VBF_LIB="$ROOT/velarixdb_amd/libvbf_seg19.so" python bench.py --no-cpu-baseline ;;
-    testseg19) run pytest_seg19 900 env VBF_LIB="$ROOT/velarixdb_amd/libvbf_seg19.so" python -m pytest tests -x -q -m gpu -k "build or config or partition" ;;
+    ablate) run ablate 300 python tools/ablate.py ;;
     benchatomic) run bench_atomic 300 python bench.py --no-cpu-baseline --strategy 1 --steps 3 ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
     bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;

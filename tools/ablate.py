@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Phase ablation of the partitioned build (timing only; results are wrong with VBF_ABLATE>0).
+
+Runs the config-2 build in child processes with VBF_ABLATE=0/1/2 and prints the library's
+per-phase hipEvent timings: 0 = full build, 1 = hash + count + scan (no place/copy),
+2 = hash only (no LDS count either)."""
+import json
+import os
+import subprocess
+import sys
+
+CHILD = r"""
+import ctypes, json, os, sys, torch
+sys.path.insert(0, os.environ["ROOT"])
+import velarixdb_amd as vbf
+from velarixdb_amd._lib import call, lib, profile_read
+n, L, m, k = 100_000_000, 16, 1_000_000_000, 10
+dev = torch.device("cuda:0")
+sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+keys = torch.empty(n * L, dtype=torch.uint8, device=dev)
+call("vbf_gen_fixed_dev", 0x5EED0001, 0, n, L, ctypes.c_void_p(keys.data_ptr()), sp)
+words = torch.zeros((m + 31) // 32, dtype=torch.int32, device=dev)
+def run():
+    call("vbf_build_dev_ex", ctypes.c_void_p(keys.data_ptr()), None, L, n, 1, m, k,
+         ctypes.c_void_p(words.data_ptr()), 2, sp)
+for _ in range(2): run()
+torch.cuda.synchronize()
+lib.vbf_profile_enable(1); profile_read()
+for _ in range(5): run()
+torch.cuda.synchronize()
+ph = profile_read()
+print(json.dumps({p: round(ms / max(c, 1), 3) for p, (ms, c) in ph.items() if c}))
+"""
+
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for a in ("0", "1", "2"):
+    env = dict(os.environ, VBF_ABLATE=a, ROOT=root)
+    out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    print("VBF_ABLATE=%s" % a, line[-1] if line else out.stderr[-2000:], flush=True)

@@ -60,6 +60,7 @@ struct PartPlan {
     uint32_t tile_words;  // u32 words per tile in the workspace: CP/2 (lo16) + CP/8 (nibbles)
     uint32_t lds1;        // K1 dynamic LDS bytes
     uint32_t stagger_lo, stagger_hi, stagger_sleeps;
+    uint32_t ablate;      // timing experiments only (VBF_ABLATE): 1 skip place+copy, 2 also count
     uint64_t m, mu, nwords;
 };
 
@@ -168,6 +169,12 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     __syncthreads();
     block_exclusive_scan(cnt, pl.nseg, wsum);
     __syncthreads();
+    if (pl.ablate) {  // timing experiment: keep the stash live, skip the sort
+        uint32_t acc = 0;
+        for (uint32_t t = 0; t < ns; ++t) acc ^= stash[t];
+        if (acc == 0x12345678u) ends[blockIdx.x] = (uint16_t)acc;
+        return;
+    }
     // rank + place, 8 returning LDS atomics in flight before their results are used
 #pragma unroll
     for (uint32_t t = 0; t < ns; t += 8) {
@@ -390,6 +397,8 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.stagger_lo = 256;
     pl.stagger_hi = 512;
     pl.stagger_sleeps = sleeps;
+    static const int abl = [] { const char* e = getenv("VBF_ABLATE"); return e ? atoi(e) : 0; }();
+    pl.ablate = (uint32_t)abl;
     return pl;
 }
 
