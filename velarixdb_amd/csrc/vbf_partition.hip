@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
-                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    if (pl.ablate != 2) atomicAdd(&cnt[idx >> kSegBits], 1u);
                 }
                 stash[r * K + i] = idx;
             }
@@ -238,7 +238,11 @@ __global__ __launch_bounds__(256) void k_transpose_u16(const uint16_t* in, uint1
 }
 
 // OR 8 packed indices (8 u16 low halves + their 8 nibbles) into the segment bitmap.
-__device__ __forceinline__ void or8(uint32_t* bitmap, uint4 l, uint32_t nib, uint32_t valid) {
+__device__ __forceinline__ void or8(uint32_t* bitmap, uint4 l, uint32_t nib, uint32_t valid, uint32_t abl = 0) {
+    if (abl == 3) {  // timing experiment: consume the loads without touching LDS
+        if ((l.x ^ l.y ^ l.z ^ l.w ^ nib) == 0x12345678u && valid == 9) bitmap[0] = 1;
+        return;
+    }
     const uint32_t w[4] = {l.x, l.y, l.z, l.w};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -320,7 +324,12 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
         for (int g = 0; g < 8; ++g) {
             if (q8 < len[g]) {
                 const uint32_t* tile = tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words;
-                load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
+                if (pl.ablate == 4) {  // timing experiment: synthetic indices, no tile loads
+                    l[g] = make_uint4(tg * 2654435761u + g, lane * 40503u, tg ^ lane, g * 977u);
+                    nib[g] = tg + lane;
+                } else {
+                    load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
+                }
             }
         }
         const uint32_t tn = tg + step;
@@ -328,7 +337,7 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
         bounds(tn, st2, len2);
 #pragma unroll
         for (int g = 0; g < 8; ++g)
-            if (q8 < len[g]) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len[g] - q8));
+            if (q8 < len[g]) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len[g] - q8), pl.ablate);
         // tail: runs longer than 64 indices (rare at the default plan; common for tiny m)
 #pragma unroll 1
         for (int g = 0; g < 8; ++g) {
