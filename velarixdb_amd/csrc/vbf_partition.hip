@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
-                    if (pl.ablate != 2) atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    if (pl.ablate != 2) if (pl.ablate != 2) atomicAdd(&cnt[idx >> kSegBits], 1u);
                 }
                 stash[r * K + i] = idx;
             }
