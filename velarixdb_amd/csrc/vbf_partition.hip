@@ -60,7 +60,6 @@ struct PartPlan {
     uint32_t tile_words;  // u32 words per tile in the workspace: CP/2 (lo16) + CP/8 (nibbles)
     uint32_t lds1;        // K1 dynamic LDS bytes
     uint32_t stagger_lo, stagger_hi, stagger_sleeps;
-    uint32_t ntiles;      // tiles in the current chunk (K1 walks them persistently)
     uint32_t ablate;      // timing experiments only (VBF_ABLATE): 1 skip place+copy, 2 also count
     uint64_t m, mu, nwords;
 };
@@ -121,15 +120,12 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     if (blockIdx.x >= pl.stagger_lo && blockIdx.x < pl.stagger_hi) {
         for (uint32_t i = 0; i < pl.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
     }
-    // Persistent: the grid is ~2 workgroups per CU and each walks tiles blockIdx, +gridDim, ...
-  for (uint32_t tile = blockIdx.x; tile < pl.ntiles; tile += gridDim.x) {
-    __syncthreads();  // LDS of the previous tile fully consumed
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
     for (uint32_t w = tid; w < pl.CP / 8; w += kPBlock) hi[w] = 0;
     __syncthreads();
 
     uint32_t stash[kStash];
-    const uint64_t key0 = (uint64_t)tile * pl.KT;
+    const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
     const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
     uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     if constexpr (K > 0) {
@@ -145,7 +141,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
-                    if (pl.ablate != 2) atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    if (pl.ablate != 2) if (pl.ablate != 2) atomicAdd(&cnt[idx >> kSegBits], 1u);
                 }
                 stash[r * K + i] = idx;
             }
@@ -173,11 +169,11 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     __syncthreads();
     block_exclusive_scan(cnt, pl.nseg, wsum);
     __syncthreads();
-    if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
+    if (pl.ablate) {  // timing experiment: keep the stash live, skip the sort
         uint32_t acc = 0;
         for (uint32_t t = 0; t < ns; ++t) acc ^= stash[t];
-        if (acc == 0x12345678u) ends[tile] = (uint16_t)acc;
-        continue;
+        if (acc == 0x12345678u) ends[blockIdx.x] = (uint16_t)acc;
+        return;
     }
     // rank + place, 8 returning LDS atomics in flight before their results are used
 #pragma unroll
@@ -209,7 +205,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     }
     __syncthreads();
     const uint32_t total = (cnt[pl.nseg - 1] + 1) & ~1u;
-    uint32_t* out = tiles + (uint64_t)tile * pl.tile_words;
+    uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.tile_words;
     const uint32_t lo_words = total / 2;
     for (uint32_t w = tid * 4; w < lo_words; w += kPBlock * 4) {
         if (w + 4 <= lo_words)
@@ -220,9 +216,8 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     uint32_t* out_hi = out + pl.CP / 2;
     const uint32_t hi_words = (total + 7) / 8;
     for (uint32_t w = tid; w < hi_words; w += kPBlock) out_hi[w] = hi[w];
-    uint16_t* eo = ends + (uint64_t)tile * pl.nseg;
+    uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nseg;
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)((cnt[s] + 1) & ~1u);
-  }
 }
 
 // ends[rows][cols] -> endsT[cols][rows], 64x64 tiles through LDS.
@@ -416,20 +411,6 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     return pl;
 }
 
-// K1 grid: two resident workgroups per CU walking the tiles (VBF_PERSIST=0: one per tile).
-static uint32_t k1_grid(uint32_t ntiles) {
-    static const int persist = [] { const char* e = getenv("VBF_PERSIST"); return e ? atoi(e) : 1; }();
-    static const uint32_t cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return (uint32_t)n;
-    }();
-    if (!persist) return ntiles;
-    return std::min<uint32_t>(ntiles, 2 * cus);
-}
-
 bool partition_supported(uint32_t m, uint32_t k) {
     if (m == 0 || k < 1 || k > (uint32_t)kStash) return false;
     const PartPlan pl = make_plan(m, k);
@@ -469,7 +450,6 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         else
             dk.keys = kb.keys + lo * kb.stride;
         const uint32_t ntiles = (uint32_t)((cn + pl.KT - 1) / pl.KT);
-        pl.ntiles = ntiles;
         hipError_t err = hipSuccess;
         phase_begin(kPhaseTileSort, s);
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
@@ -481,7 +461,7 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
             err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
             if (err == hipSuccess)
-                hipLaunchKernelGGL(fn, dim3(k1_grid(ntiles)), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
+                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
         });
         if (err != hipSuccess) return err;
         phase_end(kPhaseTileSort, s);
