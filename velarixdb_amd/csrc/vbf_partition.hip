@@ -141,7 +141,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
-                    if (pl.ablate != 2) if (pl.ablate != 2) atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    if (pl.ablate != 2) atomicAdd(&cnt[idx >> kSegBits], 1u);
                 }
                 stash[r * K + i] = idx;
             }
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     __syncthreads();
     block_exclusive_scan(cnt, pl.nseg, wsum);
     __syncthreads();
-    if (pl.ablate) {  // timing experiment: keep the stash live, skip the sort
+    if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
         uint32_t acc = 0;
         for (uint32_t t = 0; t < ns; ++t) acc ^= stash[t];
         if (acc == 0x12345678u) ends[blockIdx.x] = (uint16_t)acc;
