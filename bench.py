@@ -343,6 +343,60 @@ def bench_e2e(ctx, args):
             "dtype": "u64", "data": "synthetic", "config": {"workload": "config2 e2e %dM x 16B, filter %d words" % (n // 10**6, w.size)}}
 
 
+def bench_sst(ctx, args):
+    """the lazy filter rebuild of range.rs:117-128 from a config-2 SST --
+    data.db decode (fs/mod.rs:275-332) alone, and decode + build fused
+    (vbf_filter_rebuild_from_sst_dev).  data.db is device-resident (as a GPU-direct read would
+    leave it); each step includes the decoder's one entry-count readback."""
+    n, L = args.keys, 16
+    per = 4096 // (L + 17)
+    nb = (n + per - 1) // per
+    data = torch.empty(n * (L + 17), dtype=torch.uint8, device=ctx.dev)
+    blocks = torch.empty(nb, dtype=torch.int32, device=ctx.dev)
+    call("vbf_gen_sst_fixed_dev", wl.SEED_CFG2, 0, n, L, vp(data), vp(blocks), ctx.sp)
+    out_k = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
+    out_o = torch.empty(n + 1, dtype=torch.int64, device=ctx.dev)
+    got = ctypes.c_uint64()
+
+    def decode(evs):
+        call("vbf_sst_decode_dev", vp(data), data.numel(), vp(blocks), nb, vp(out_k), out_k.numel(), vp(out_o),
+             None, None, None, n + 1, ctypes.byref(got), ctx.sp)
+
+    dwall, _, dph = timed_steps(ctx, decode, args.steps, args.warmup)
+    assert got.value == n
+    p = wl.fpr_for_bits_per_key(10)
+    bf = vbf.BloomFilter(p, n, device=ctx.local)
+
+    def rebuild(evs):
+        bf.rebuild_from_sst_dev(vp(data), data.numel(), vp(blocks), nb, ctx.sp)
+
+    rwall, _, rph = timed_steps(ctx, rebuild, args.steps, args.warmup)
+    res = {"metric": "SST filter rebuild keys/s (data.db decode + build, device-resident data.db)",
+           "value": ctx.sum_over_ranks(n) * args.steps / rwall, "unit": "keys/s", "n_gpus": ctx.world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": rwall / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "data": "synthetic",
+           "config": {"workload": "config2 SST: %dM x 16B keys in data.db (%.2f GB, %d blocks), m=%d, k=%d"
+                      % (n // 10**6, data.numel() / 1e9, nb, bf.num_bits(), bf.no_of_hash_func)},
+           "decode_only": {"ms_per_step": dwall / args.steps * 1e3,
+                           "entries_per_s": n * args.steps / dwall,
+                           "data_gb_per_s": data.numel() * args.steps / dwall / 1e9},
+           "phases": phase_report(rph, args.steps)}
+    if ctx.world == 1 and ctx.rank == 0 and not args.no_cpu_baseline:
+        import oracle
+        ns = min(n, args.cpu_sample)
+        host = data[: ns * (L + 17)].cpu().numpy()
+        t0 = time.perf_counter()
+        keys, offs, *_ = oracle.sst_decode(host)
+        from velarixdb_amd.keys import HostBatch
+        oracle.build_words(HostBatch(keys, offs, 0, ns, 1), bf.num_bits(), bf.no_of_hash_func)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": ns / dt, "unit": "keys/s", "cores": 1, "kind": "port",
+                               "sample": "first %d entries of the same data.db: load_entries + build" % ns,
+                               "seconds": round(dt, 3)}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -354,6 +408,7 @@ def main():
     ap.add_argument("--bits-per-key", type=int, default=10)
     ap.add_argument("--neg-keys", type=int, default=None)
     ap.add_argument("--e2e", action="store_true")
+    ap.add_argument("--sst", action="store_true", help="SST data.db decode + rebuild (8(f) row 2)")
     ap.add_argument("--strategy", type=int, default=0, help="0 auto, 1 atomic, 2 partitioned")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
@@ -368,6 +423,9 @@ def main():
         args.keys = args.keys or 100_000_000
         args.neg_keys = args.neg_keys or 50_000_000
         res = bench_var(ctx, args)
+    elif args.sst:
+        args.keys = args.keys or 100_000_000
+        res = bench_sst(ctx, args)
     elif args.e2e:
         args.keys = args.keys or 100_000_000
         res = bench_e2e(ctx, args)

@@ -21,6 +21,9 @@
  *   calculate_no_of_hash_function      src/filter/bf.rs:236-239    -> vbf_num_hash_functions
  *   Clone (shares the bit array)       src/filter/bf.rs:242-254    -> vbf_filter_clone
  *   Default                            src/filter/bf.rs:256-267    -> vbf_filter_default
+ *   DataFileNode::load_entries         src/fs/mod.rs:275-332       -> vbf_sst_decode_dev / _host
+ *   index.db block offsets             src/index/indexer.rs:151-170 -> vbf_sst_index_blocks
+ *   lazy filter rebuild                src/key_range/range.rs:117-128 -> vbf_filter_rebuild_from_sst_*
  *
  * Key batches.  `keys` holds the key bytes back to back.  When `offsets` is non-NULL it has
  * n+1 nondecreasing entries and key j is keys[offsets[j] .. offsets[j+1]) (positions are
@@ -157,6 +160,54 @@ int vbf_filter_clear(vbf_filter* f, vbf_filter** out);
 /* Bit-array persistence: copy the ceil(m/32) words out / in. */
 int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords);
 int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nwords);
+
+/* Synthetic data.db (bench / tests): n entries whose keys are vbf_gen_fixed_dev's, value offset
+ * (u32)j, created_at 1720785462000 + j ms, tombstone j % 97 == 0, blocked as
+ * Table::write_to_file blocks them (src/sst/table.rs:295-324): floor(4096 / (len + 17)) entries
+ * per block.  data: n * (len + 17) bytes; blocks: ceil(n / per_block) u32 start offsets. */
+int vbf_gen_sst_fixed_dev(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* data,
+                          uint32_t* blocks, void* stream);
+
+/* ---- SST data.db decode ----
+ * data.db = blocks of whole entries, entry = u32 key_len | key | u32 value offset | i64
+ * created_at ms | u8 tombstone (src/block/block_manager.rs:168-190), each block <= 4096 bytes
+ * (:121-125); index.db holds one u32 key_len | key | u32 block offset record per block
+ * (src/index/indexer.rs:151-170).  The decode is block-parallel, so it needs the block offsets. */
+
+/* index.db bytes -> block start offsets.  Writes min(cap, count) offsets (offsets may be NULL)
+ * and the count to *nblocks; VBF_EINVAL on a truncated record.  Host-only. */
+int vbf_sst_index_blocks(const uint8_t* index, uint64_t len, uint32_t* offsets, uint64_t cap,
+                         uint64_t* nblocks);
+
+/* DataFileNode::load_entries (src/fs/mod.rs:275-332) on the device.  data/blocks are device
+ * pointers; outputs are device pointers, each may be NULL: keys (packed key bytes, 4-byte aligned,
+ * keys_cap >= len - 17 n), offsets (n+1 absolute positions in keys: the build's key layout),
+ * val_offsets, created_ms, tombstones (1 iff the byte is 1, as the reference reads it),
+ * entries_cap >= n (+1 for offsets).  *n_out = entry count, also when the outputs are too small
+ * (VBF_EINVAL) so a first call with NULL outputs sizes them.  Synchronizes the stream once (the
+ * entry count); the output pass is left queued on it.  A malformed file (entry crossing its block,
+ * offsets out of order) is VBF_EINVAL, where the reference reports UnexpectedEof. */
+int vbf_sst_decode_dev(const uint8_t* data, uint64_t len, const uint32_t* blocks, uint64_t nblocks,
+                       uint8_t* keys, uint64_t keys_cap, uint64_t* offsets, uint32_t* val_offsets,
+                       uint64_t* created_ms, uint8_t* tombstones, uint64_t entries_cap,
+                       uint64_t* n_out, void* stream);
+
+/* Same from host buffers (the data.db and index.db file contents) to host outputs; decoded on
+ * `device`.  Synchronous. */
+int vbf_sst_decode_host(const uint8_t* data, uint64_t len, const uint8_t* index, uint64_t index_len,
+                        uint8_t* keys, uint64_t keys_cap, uint64_t* offsets, uint32_t* val_offsets,
+                        uint64_t* created_ms, uint8_t* tombstones, uint64_t entries_cap,
+                        uint64_t* n_out, int device);
+
+/* The lazy rebuild of src/key_range/range.rs:117-128 (load_entries_from_file then
+ * build_filter_from_entries): decode data.db on the filter's device and OR every key into its
+ * bits (len_prefix = 1), no_of_elements += n.  *n_out (may be NULL) = entries decoded.
+ * _dev: device data/blocks, queued on `stream` after one count readback.  _host: file bytes. */
+int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t len,
+                                    const uint32_t* blocks, uint64_t nblocks, uint64_t* n_out,
+                                    void* stream);
+int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_t len,
+                                     const uint8_t* index, uint64_t index_len, uint64_t* n_out);
 
 #ifdef __cplusplus
 }

@@ -50,6 +50,12 @@ def _load():
     L.ora_gen_var_len.argtypes = [u64, u64]
     L.ora_gen_var.restype = None
     L.ora_gen_var.argtypes = [u64, u64, u64, vp, vp]
+    L.ora_sst_write.restype = i
+    L.ora_sst_write.argtypes = [vp, vp, u64, vp, vp, vp, vp, vp, vp, vp]
+    L.ora_sst_decode.restype = ctypes.c_int64
+    L.ora_sst_decode.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+    L.ora_sst_index_blocks.restype = ctypes.c_int64
+    L.ora_sst_index_blocks.argtypes = [vp, u64, vp]
     return L
 
 
@@ -127,3 +133,50 @@ def gen_var(seed, base, offsets):
     out = np.zeros(int(offsets[-1]), dtype=np.uint8)
     lib.ora_gen_var(seed, base, n, offsets.ctypes.data, out.ctypes.data if out.size else None)
     return out
+
+
+def _p(a):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+def sst_write(keys, offsets, val_off=None, created_ms=None, tomb=None):
+    """Table::write_to_file (table.rs:280-338) -> (data.db bytes, index.db bytes)."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    arrs = [None if a is None else np.ascontiguousarray(a, dtype=t)
+            for a, t in ((val_off, np.uint32), (created_ms, np.uint64), (tomb, np.uint8))]
+    dl, il = ctypes.c_uint64(), ctypes.c_uint64()
+    args = [_p(keys), _p(offsets), n] + [_p(a) for a in arrs]
+    if lib.ora_sst_write(*args, None, ctypes.byref(dl), None, ctypes.byref(il)) != 0:
+        raise ValueError("entry larger than a 4096-byte block (BlockIsFull)")
+    data = np.zeros(dl.value, dtype=np.uint8)
+    index = np.zeros(il.value, dtype=np.uint8)
+    lib.ora_sst_write(*args, _p(data), ctypes.byref(dl), _p(index), ctypes.byref(il))
+    return data, index
+
+
+def sst_decode(data):
+    """DataFileNode::load_entries (fs/mod.rs:275-332) -> (keys, offsets, val_off, created_ms, tomb)."""
+    data = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    n = lib.ora_sst_decode(_p(data), data.size, None, None, None, None, None)
+    if n < 0:
+        raise EOFError("unexpected EOF in data.db")
+    keys = np.zeros(data.size - 17 * n, dtype=np.uint8)
+    offsets = np.zeros(n + 1, dtype=np.uint64)
+    val = np.zeros(n, dtype=np.uint32)
+    created = np.zeros(n, dtype=np.uint64)
+    tomb = np.zeros(n, dtype=np.uint8)
+    lib.ora_sst_decode(_p(data), data.size, _p(keys), offsets.ctypes.data, _p(val), _p(created), _p(tomb))
+    return keys, offsets, val, created, tomb
+
+
+def sst_index_blocks(index):
+    """index.db (indexer.rs:151-170) -> u32 block start offsets."""
+    index = np.frombuffer(bytes(index), dtype=np.uint8) if not isinstance(index, np.ndarray) else index
+    nb = lib.ora_sst_index_blocks(_p(index), index.size, None)
+    if nb < 0:
+        raise EOFError("unexpected EOF in index.db")
+    offs = np.zeros(nb, dtype=np.uint32)
+    lib.ora_sst_index_blocks(_p(index), index.size, _p(offs))
+    return offs

@@ -301,3 +301,108 @@ void ora_gen_var(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offse
         }
     }
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * SST data.db / index.db: the step before the build on the recovery path.
+ * ------------------------------------------------------------------------------------------- */
+
+#define SST_BLOCK_SIZE 4096u /* consts/mod.rs:107 */
+#define SST_ENTRY_FIXED 17u  /* u32 key_len + u32 value offset + u64 created_at + u8 tombstone */
+
+static void put_le(uint8_t* p, uint64_t v, int nbytes) {
+    for (int i = 0; i < nbytes; ++i) p[i] = (uint8_t)(v >> (8 * i));
+}
+static uint64_t get_le(const uint8_t* p, int nbytes) {
+    uint64_t v = 0;
+    for (int i = 0; i < nbytes; ++i) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+}
+
+/* Table::write_to_file (sst/table.rs:280-324) with Block::set_entry / is_full
+ * (block/block_manager.rs:112-139: a block takes an entry unless size + (L + 17) > 4096, so an
+ * entry over 4096 bytes fails the flush), Block::serialize (:168-190: u32 key_len | key |
+ * u32 value offset | i64 created_at ms | u8 tombstone), write_block (table.rs:331-338: one index
+ * entry per block = its LAST key and the block's start offset) and Index::serialize_entry
+ * (index/indexer.rs:151-170: u32 key_len | key | u32 block offset).
+ * data / index may be NULL to size the files.  Returns 0, or -1 when an entry exceeds a block. */
+int ora_sst_write(const uint8_t* keys, const uint64_t* offsets, uint64_t n, const uint32_t* val_off,
+                  const uint64_t* created_ms, const uint8_t* tomb, uint8_t* data, uint64_t* data_len,
+                  uint8_t* index, uint64_t* index_len) {
+    uint64_t dpos = 0, ipos = 0, blk_start = 0, blk_size = 0;
+    int64_t last = -1; /* last entry of the open block */
+    for (uint64_t j = 0; j <= n; ++j) {
+        uint64_t es = 0;
+        if (j < n) {
+            es = (offsets[j + 1] - offsets[j]) + SST_ENTRY_FIXED;
+            if (es > SST_BLOCK_SIZE) return -1;
+        }
+        if (last >= 0 && (j == n || blk_size + es > SST_BLOCK_SIZE)) { /* close the block */
+            uint64_t L = offsets[last + 1] - offsets[last];
+            if (index) {
+                put_le(index + ipos, L, 4);
+                memcpy(index + ipos + 4, keys + offsets[last], L);
+                put_le(index + ipos + 4 + L, blk_start, 4);
+            }
+            ipos += L + 8;
+            blk_start = dpos;
+            blk_size = 0;
+            last = -1;
+        }
+        if (j == n) break;
+        uint64_t L = es - SST_ENTRY_FIXED;
+        if (data) {
+            put_le(data + dpos, L, 4);
+            memcpy(data + dpos + 4, keys + offsets[j], L);
+            put_le(data + dpos + 4 + L, val_off ? val_off[j] : 0, 4);
+            put_le(data + dpos + 8 + L, created_ms ? created_ms[j] : 0, 8);
+            data[dpos + 16 + L] = tomb ? (tomb[j] != 0) : 0;
+        }
+        dpos += es;
+        blk_size += es;
+        last = (int64_t)j;
+    }
+    *data_len = dpos;
+    *index_len = ipos;
+    return 0;
+}
+
+/* DataFileNode::load_entries (fs/mod.rs:275-332): sequential entries until EOF.  Output arrays
+ * may be NULL (count only); offsets gets n+1 entries (absolute positions in keys).  tomb[j] =
+ * (byte == 1) as the reference reads it.  Returns the entry count, or -1 on a truncated entry
+ * (the reference's UnexpectedEof). */
+int64_t ora_sst_decode(const uint8_t* data, uint64_t len, uint8_t* keys, uint64_t* offsets,
+                       uint32_t* val_off, uint64_t* created_ms, uint8_t* tomb) {
+    uint64_t p = 0, kb = 0;
+    int64_t n = 0;
+    while (p < len) {
+        if (len - p < 4) return -1;
+        uint64_t L = get_le(data + p, 4);
+        if (len - p - 4 < L + 13) return -1;
+        if (keys) memcpy(keys + kb, data + p + 4, L);
+        if (offsets) offsets[n] = kb;
+        if (val_off) val_off[n] = (uint32_t)get_le(data + p + 4 + L, 4);
+        if (created_ms) created_ms[n] = get_le(data + p + 8 + L, 8);
+        if (tomb) tomb[n] = data[p + 16 + L] == 1;
+        kb += L;
+        p += L + SST_ENTRY_FIXED;
+        ++n;
+    }
+    if (offsets) offsets[n] = kb;
+    return n;
+}
+
+/* index.db (indexer.rs:151-170) -> block start offsets.  offs may be NULL (count only).
+ * Returns the block count, or -1 on a truncated entry. */
+int64_t ora_sst_index_blocks(const uint8_t* index, uint64_t len, uint32_t* offs) {
+    uint64_t p = 0;
+    int64_t nb = 0;
+    while (p < len) {
+        if (len - p < 4) return -1;
+        uint64_t L = get_le(index + p, 4);
+        if (len - p - 4 < L + 4) return -1;
+        if (offs) offs[nb] = (uint32_t)get_le(index + p + 4 + L, 4);
+        p += L + 8;
+        ++nb;
+    }
+    return nb;
+}

@@ -64,6 +64,17 @@ void ora_gen_fixed(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8
 uint32_t ora_gen_var_len(uint64_t seed, uint64_t j);
 void ora_gen_var(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offsets, uint8_t* out);
 
+
+/* SST files, see oracle.c for the reference anchors:
+ * writer (table.rs:280-338, block_manager.rs:112-190, indexer.rs:130-170), data.db decoder
+ * (fs/mod.rs:275-332) and index.db -> block start offsets. */
+int ora_sst_write(const uint8_t* keys, const uint64_t* offsets, uint64_t n, const uint32_t* val_off,
+                  const uint64_t* created_ms, const uint8_t* tomb, uint8_t* data, uint64_t* data_len,
+                  uint8_t* index, uint64_t* index_len);
+int64_t ora_sst_decode(const uint8_t* data, uint64_t len, uint8_t* keys, uint64_t* offsets,
+                       uint32_t* val_off, uint64_t* created_ms, uint8_t* tomb);
+int64_t ora_sst_index_blocks(const uint8_t* index, uint64_t len, uint32_t* offs);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,7 @@ for s in $STEPS; do
     benchatomic) run bench_atomic 300 python bench.py --no-cpu-baseline --strategy 1 --steps 3 ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
     bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;
+    sst)    run bench_sst 600 python bench.py --sst --steps 5 --warmup 1 ;;
     e2e)    run bench_e2e 600 python bench.py --e2e --steps 3 --warmup 1 ;;
     ubench) run ubench 300 ./tools/ubench ;;
     counters) (cd /tmp && run counters 120 rocprofv3 -L) || exit $? ;;

@@ -4,7 +4,9 @@
 Runs the config-2 build in child processes with VBF_ABLATE=0/1/2 and prints the library's
 per-phase hipEvent timings: 0 = full build, 1 = hash + count + scan (no place/copy),
 2 = hash only (no LDS count either), 3 = seg_or loads without ds_or, 4 = seg_or ds_or on
-synthetic indices without tile loads."""
+synthetic indices without tile loads,
+5 = seg_or without its tile loop (word load + LDS init + write-back), 6 = also without the word
+load, 7 = LDS init only."""
 import json
 import os
 import subprocess
@@ -34,7 +36,7 @@ print(json.dumps({p: round(ms / max(c, 1), 3) for p, (ms, c) in ph.items() if c}
 """
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for a in ("0", "1", "2", "3", "4"):
+for a in ("0", "1", "2", "3", "4", "5", "6", "7"):
     env = dict(os.environ, VBF_ABLATE=a, ROOT=root)
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]

@@ -73,6 +73,12 @@ SIGNATURES = {
     "vbf_filter_clear": (_int, [_vp, ctypes.POINTER(_vp)]),
     "vbf_filter_words_to_host": (_int, [_vp, _vp, _u64]),
     "vbf_filter_words_from_host": (_int, [_vp, _vp, _u64]),
+    "vbf_gen_sst_fixed_dev": (_int, [_u64, _u64, _u64, _u32, _vp, _vp, _vp]),
+    "vbf_sst_index_blocks": (_int, [_vp, _u64, _vp, _u64, _vp]),
+    "vbf_sst_decode_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
+    "vbf_sst_decode_host": (_int, [_vp, _u64, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp, _int]),
+    "vbf_filter_rebuild_from_sst_dev": (_int, [_vp, _vp, _u64, _vp, _u64, _vp, _vp]),
+    "vbf_filter_rebuild_from_sst_host": (_int, [_vp, _vp, _u64, _vp, _u64, _vp]),
 }
 
 

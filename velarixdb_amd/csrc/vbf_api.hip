@@ -97,21 +97,24 @@ vbf::KeyBatch batch(const uint8_t* keys, const uint64_t* offsets, uint64_t off_b
 // Partitioned-build workspace: one grow-only buffer per (device, stream), so concurrent
 // builds on different streams never share scratch.
 // ---------------------------------------------------------------------------------------
+enum WsSlot { kWsBuild = 0, kWsSstScratch = 1, kWsSstKeys = 2, kWsSstInput = 3 };
 struct Workspace {
     int device;
     hipStream_t stream;
+    int slot;
     void* ptr;
     uint64_t bytes;
 };
 std::mutex g_ws_mu;
 std::vector<Workspace> g_ws;
 
-int get_workspace(hipStream_t s, uint64_t bytes, void** out) {
+int get_workspace(hipStream_t s, uint64_t bytes, void** out, int slot = kWsBuild) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
+    bytes = std::max<uint64_t>(bytes, 256);
     std::lock_guard<std::mutex> lk(g_ws_mu);
     for (auto& w : g_ws) {
-        if (w.device == dev && w.stream == s) {
+        if (w.device == dev && w.stream == s && w.slot == slot) {
             if (w.bytes < bytes) {
                 HIP_TRY(hipStreamSynchronize(s));  // the old buffer may still be in use on s
                 HIP_TRY(hipFree(w.ptr));
@@ -126,7 +129,7 @@ int get_workspace(hipStream_t s, uint64_t bytes, void** out) {
     }
     void* p = nullptr;
     HIP_TRY(hipMalloc(&p, bytes));
-    g_ws.push_back(Workspace{dev, s, p, bytes});
+    g_ws.push_back(Workspace{dev, s, slot, p, bytes});
     *out = p;
     return VBF_OK;
 }
@@ -373,6 +376,92 @@ void phase_end(int phase, hipStream_t s) {
 }  // namespace vbf
 
 namespace {
+
+// ---------------------------------------------------------------------------------------
+// SST data.db decode (vbf_sst.hip): count pass + scan, one 16-byte readback (entry total and
+// error word) so the caller can size or validate, then the emit pass queued on the stream.
+// ---------------------------------------------------------------------------------------
+inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+
+int sst_count_pass(const uint8_t* data, uint64_t len, const uint32_t* blocks, uint64_t nblocks,
+                   hipStream_t s, vbf::SstArgs* a, uint64_t* n_out) {
+    *a = vbf::SstArgs{};
+    *n_out = 0;
+    if (len && (!data || !blocks || !nblocks))
+        return fail(VBF_EINVAL, "data.db of %llu bytes needs its block start offsets (index.db)",
+                    (unsigned long long)len);
+    if (!len && nblocks) return fail(VBF_EINVAL, "%llu block offsets for an empty data.db", (unsigned long long)nblocks);
+    if (nblocks >= 0x7FFFFFFFull) return fail(VBF_EINVAL, "too many blocks (%llu)", (unsigned long long)nblocks);
+    if (!len) return VBF_OK;
+    size_t tmpb = 0;
+    HIP_TRY(vbf::sst_scan(nullptr, nullptr, nblocks + 1, nullptr, &tmpb, s));
+    const uint64_t o_ebase = align256((nblocks + 1) * 4);
+    const uint64_t o_err = o_ebase + align256((nblocks + 1) * 8);
+    const uint64_t o_tmp = o_err + 256;
+    void* ws = nullptr;
+    int rc = get_workspace(s, o_tmp + tmpb, &ws, kWsSstScratch);
+    if (rc) return rc;
+    char* base = static_cast<char*>(ws);
+    uint32_t* counts = reinterpret_cast<uint32_t*>(base);
+    uint64_t* ebase = reinterpret_cast<uint64_t*>(base + o_ebase);
+    uint32_t* err = reinterpret_cast<uint32_t*>(base + o_err);
+    HIP_TRY(hipMemsetAsync(counts, 0, (nblocks + 1) * 4, s));
+    HIP_TRY(hipMemsetAsync(err, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(err + 1, 0xFF, 4, s));
+    *a = vbf::SstArgs{data, len, blocks, nblocks, counts, ebase, nullptr, nullptr, nullptr, nullptr, nullptr, err};
+    HIP_TRY(vbf::sst_count(*a, s));
+    HIP_TRY(vbf::sst_scan(counts, ebase, nblocks + 1, base + o_tmp, &tmpb, s));
+    uint64_t total = 0;
+    uint32_t ev[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&total, ebase + nblocks, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(ev, err, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ev[0]) {
+        const char* what = (ev[0] & 8) ? "block offsets not increasing / not starting at 0 / past the end"
+                         : (ev[0] & 4) ? "block larger than 8192 bytes"
+                         : (ev[0] & 2) ? "more than 512 entries in a block"
+                                       : "entry crosses the block end (truncated data.db or wrong index)";
+        return fail(VBF_EINVAL, "malformed data.db at block %u: %s", ev[1], what);
+    }
+    if (len < 17 * total) return fail(VBF_EINVAL, "inconsistent entry count %llu", (unsigned long long)total);
+    *n_out = total;
+    return VBF_OK;
+}
+
+int sst_emit_pass(vbf::SstArgs a, uint8_t* keys, uint64_t* offsets, uint32_t* val_off, uint64_t* created,
+                  uint8_t* tomb, hipStream_t s) {
+    if (!a.len) {
+        if (offsets) HIP_TRY(hipMemsetAsync(offsets, 0, 8, s));
+        return VBF_OK;
+    }
+    if (keys && ((uintptr_t)keys & 3)) return fail(VBF_EINVAL, "keys buffer must be 4-byte aligned");
+    a.keys = keys;
+    a.offsets = offsets;
+    a.val_off = val_off;
+    a.created = created;
+    a.tomb = tomb;
+    if (!keys && !offsets && !val_off && !created && !tomb) return VBF_OK;
+    HIP_TRY(vbf::sst_emit(a, s));
+    return VBF_OK;
+}
+
+// index.db (indexer.rs:151-170: u32 key_len | key | u32 block offset per block) -> offsets.
+int parse_index(const uint8_t* index, uint64_t len, std::vector<uint32_t>* out) {
+    out->clear();
+    uint64_t p = 0;
+    while (p < len) {
+        if (len - p < 4) return fail(VBF_EINVAL, "index.db truncated at byte %llu", (unsigned long long)p);
+        uint32_t L;
+        memcpy(&L, index + p, 4);
+        if (len - p - 4 < (uint64_t)L + 4) return fail(VBF_EINVAL, "index.db truncated at byte %llu", (unsigned long long)p);
+        uint32_t off;
+        memcpy(&off, index + p + 4 + L, 4);
+        out->push_back(off);
+        p += (uint64_t)L + 8;
+    }
+    return VBF_OK;
+}
+
 }  // namespace
 
 struct vbf_filter {
@@ -561,6 +650,14 @@ int vbf_gen_var_dev(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* of
                     void* stream) {
     if (n && (!offsets || !out)) return fail(VBF_EINVAL, "NULL argument");
     HIP_TRY(vbf::launch_gen_var(seed, base, n, offsets, out, (hipStream_t)stream));
+    return ok();
+}
+
+int vbf_gen_sst_fixed_dev(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* data,
+                          uint32_t* blocks, void* stream) {
+    if (n && (!data || !blocks)) return fail(VBF_EINVAL, "NULL argument");
+    if (len + 17 > 4096) return fail(VBF_EINVAL, "an entry of %u + 17 bytes exceeds a 4096-byte block", len);
+    HIP_TRY(vbf::gen_sst_fixed(seed, base, n, len, data, blocks, (hipStream_t)stream));
     return ok();
 }
 
@@ -823,6 +920,139 @@ int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nword
     std::lock_guard<std::mutex> lk(s.mu);
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(s.d_words, in, s.nwords * 4, hipMemcpyHostToDevice));
+    return ok();
+}
+
+// ---- SST data.db decode ----
+
+int vbf_sst_index_blocks(const uint8_t* index, uint64_t len, uint32_t* offsets, uint64_t cap, uint64_t* nblocks) {
+    if (!nblocks || (len && !index)) return fail(VBF_EINVAL, "NULL argument");
+    std::vector<uint32_t> v;
+    int rc = parse_index(index, len, &v);
+    if (rc) return rc;
+    *nblocks = v.size();
+    if (offsets && cap) memcpy(offsets, v.data(), 4 * std::min<uint64_t>(cap, v.size()));
+    return ok();
+}
+
+int vbf_sst_decode_dev(const uint8_t* data, uint64_t len, const uint32_t* blocks, uint64_t nblocks, uint8_t* keys,
+                       uint64_t keys_cap, uint64_t* offsets, uint32_t* val_offsets, uint64_t* created_ms,
+                       uint8_t* tombstones, uint64_t entries_cap, uint64_t* n_out, void* stream) {
+    if (!n_out) return fail(VBF_EINVAL, "n_out is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    vbf::SstArgs a;
+    int rc = sst_count_pass(data, len, blocks, nblocks, s, &a, n_out);
+    if (rc) return rc;
+    const uint64_t n = *n_out, kb = len - 17 * n;
+    if ((val_offsets || created_ms || tombstones) && entries_cap < n)
+        return fail(VBF_EINVAL, "entry arrays hold %llu < %llu entries", (unsigned long long)entries_cap,
+                    (unsigned long long)n);
+    if (offsets && entries_cap < n + 1)
+        return fail(VBF_EINVAL, "offsets holds %llu < %llu entries", (unsigned long long)entries_cap,
+                    (unsigned long long)(n + 1));
+    if (keys && keys_cap < kb)
+        return fail(VBF_EINVAL, "keys holds %llu < %llu bytes", (unsigned long long)keys_cap, (unsigned long long)kb);
+    if ((rc = sst_emit_pass(a, keys, offsets, val_offsets, created_ms, tombstones, s))) return rc;
+    return ok();
+}
+
+int vbf_sst_decode_host(const uint8_t* data, uint64_t len, const uint8_t* index, uint64_t index_len, uint8_t* keys,
+                        uint64_t keys_cap, uint64_t* offsets, uint32_t* val_offsets, uint64_t* created_ms,
+                        uint8_t* tombstones, uint64_t entries_cap, uint64_t* n_out, int device) {
+    if (!n_out || (len && !data) || (index_len && !index)) return fail(VBF_EINVAL, "NULL argument");
+    std::vector<uint32_t> blk;
+    int rc = parse_index(index, index_len, &blk);
+    if (rc) return rc;
+    DEVICE_SCOPE(device);
+    hipStream_t s;
+    if ((rc = filter_stream(device, &s))) return rc;
+    // device image: data | blocks | then the outputs (count pass first, to size them)
+    const uint64_t o_blk = align256(len), o_end = o_blk + align256(blk.size() * 4);
+    void* in = nullptr;
+    if ((rc = get_workspace(s, o_end, &in, kWsSstInput))) return rc;
+    uint8_t* d_data = static_cast<uint8_t*>(in);
+    uint32_t* d_blk = reinterpret_cast<uint32_t*>(d_data + o_blk);
+    if (len) HIP_TRY(hipMemcpyAsync(d_data, data, len, hipMemcpyHostToDevice, s));
+    if (blk.size()) HIP_TRY(hipMemcpyAsync(d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, s));
+    vbf::SstArgs a;
+    if ((rc = sst_count_pass(d_data, len, d_blk, blk.size(), s, &a, n_out))) return rc;
+    const uint64_t n = *n_out, kb = len - 17 * n;
+    if ((val_offsets || created_ms || tombstones) && entries_cap < n)
+        return fail(VBF_EINVAL, "entry arrays hold %llu < %llu entries", (unsigned long long)entries_cap,
+                    (unsigned long long)n);
+    if (offsets && entries_cap < n + 1)
+        return fail(VBF_EINVAL, "offsets holds %llu < %llu entries", (unsigned long long)entries_cap,
+                    (unsigned long long)(n + 1));
+    if (keys && keys_cap < kb)
+        return fail(VBF_EINVAL, "keys holds %llu < %llu bytes", (unsigned long long)keys_cap, (unsigned long long)kb);
+    const uint64_t o_keys = 0, o_off = align256(kb), o_val = o_off + align256((n + 1) * 8);
+    const uint64_t o_cr = o_val + align256(n * 4), o_tb = o_cr + align256(n * 8), total = o_tb + align256(n);
+    void* out = nullptr;
+    if ((rc = get_workspace(s, total, &out, kWsSstKeys))) return rc;
+    char* ob = static_cast<char*>(out);
+    uint8_t* d_keys = keys ? reinterpret_cast<uint8_t*>(ob + o_keys) : nullptr;
+    uint64_t* d_off = offsets ? reinterpret_cast<uint64_t*>(ob + o_off) : nullptr;
+    uint32_t* d_val = val_offsets ? reinterpret_cast<uint32_t*>(ob + o_val) : nullptr;
+    uint64_t* d_cr = created_ms ? reinterpret_cast<uint64_t*>(ob + o_cr) : nullptr;
+    uint8_t* d_tb = tombstones ? reinterpret_cast<uint8_t*>(ob + o_tb) : nullptr;
+    if ((rc = sst_emit_pass(a, d_keys, d_off, d_val, d_cr, d_tb, s))) return rc;
+    if (keys && kb) HIP_TRY(hipMemcpyAsync(keys, d_keys, kb, hipMemcpyDeviceToHost, s));
+    if (offsets) HIP_TRY(hipMemcpyAsync(offsets, d_off, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (val_offsets && n) HIP_TRY(hipMemcpyAsync(val_offsets, d_val, n * 4, hipMemcpyDeviceToHost, s));
+    if (created_ms && n) HIP_TRY(hipMemcpyAsync(created_ms, d_cr, n * 8, hipMemcpyDeviceToHost, s));
+    if (tombstones && n) HIP_TRY(hipMemcpyAsync(tombstones, d_tb, n, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return ok();
+}
+
+// range.rs:117-128 (load_entries_from_file + build_filter_from_entries) on the device: decode
+// data.db into packed keys/offsets and OR their bits into the filter; no_of_elements += n.
+int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t len, const uint32_t* blocks,
+                                    uint64_t nblocks, uint64_t* n_out, void* stream) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    DEVICE_SCOPE(s.device);
+    hipStream_t st = (hipStream_t)stream;
+    uint64_t n = 0;
+    vbf::SstArgs a;
+    int rc = sst_count_pass(data, len, blocks, nblocks, st, &a, &n);
+    if (rc) return rc;
+    if (n_out) *n_out = n;
+    if ((rc = check_mk(s.m, f->k, n))) return rc;
+    if (n && f->k) {
+        const uint64_t kb = len - 17 * n, o_off = align256(kb);
+        void* out = nullptr;
+        if ((rc = get_workspace(st, o_off + (n + 1) * 8, &out, kWsSstKeys))) return rc;
+        uint8_t* d_keys = static_cast<uint8_t*>(out);
+        uint64_t* d_off = reinterpret_cast<uint64_t*>(d_keys + o_off);
+        if ((rc = sst_emit_pass(a, d_keys, d_off, nullptr, nullptr, nullptr, st))) return rc;
+        std::lock_guard<std::mutex> lk(s.mu);
+        vbf::KeyBatch kb2 = batch(d_keys, d_off, 0, 0, n, 1);
+        if ((rc = do_build(kb2, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, st))) return rc;
+    }
+    f->n.fetch_add((uint32_t)n);
+    return ok();
+}
+
+int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_t len, const uint8_t* index,
+                                     uint64_t index_len, uint64_t* n_out) {
+    if (!f || (len && !data) || (index_len && !index)) return fail(VBF_EINVAL, "NULL argument");
+    Storage& s = *f->bits;
+    std::vector<uint32_t> blk;
+    int rc = parse_index(index, index_len, &blk);
+    if (rc) return rc;
+    DEVICE_SCOPE(s.device);
+    hipStream_t st;
+    if ((rc = filter_stream(s.device, &st))) return rc;
+    const uint64_t o_blk = align256(len), o_end = o_blk + align256(blk.size() * 4);
+    void* in = nullptr;
+    if ((rc = get_workspace(st, o_end, &in, kWsSstInput))) return rc;
+    uint8_t* d_data = static_cast<uint8_t*>(in);
+    uint32_t* d_blk = reinterpret_cast<uint32_t*>(d_data + o_blk);
+    if (len) HIP_TRY(hipMemcpyAsync(d_data, data, len, hipMemcpyHostToDevice, st));
+    if (blk.size()) HIP_TRY(hipMemcpyAsync(d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
+    if ((rc = vbf_filter_rebuild_from_sst_dev(f, d_data, len, d_blk, blk.size(), n_out, st))) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
     return ok();
 }
 

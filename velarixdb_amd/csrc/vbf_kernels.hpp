@@ -45,4 +45,26 @@ hipError_t launch_gen_fixed(uint64_t seed, uint64_t base, uint64_t n, uint32_t l
 hipError_t launch_gen_var(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offsets,
                           uint8_t* out, hipStream_t s);
 
+
+// SST data.db decode (vbf_sst.hip).  Output arrays may be NULL.
+struct SstArgs {
+    const uint8_t* data;
+    uint64_t len;
+    const uint32_t* blocks;  // block start offsets (index.db)
+    uint64_t nblocks;
+    uint32_t* counts;        // [nblocks + 1] entry counts (count pass)
+    const uint64_t* ebase;   // [nblocks + 1] exclusive scan of counts (emit pass)
+    uint8_t* keys;
+    uint64_t* offsets;       // [n + 1] absolute positions in keys
+    uint32_t* val_off;
+    uint64_t* created;
+    uint8_t* tomb;
+    uint32_t* err;           // [0] error bits, [1] first bad block
+};
+hipError_t sst_count(const SstArgs& a, hipStream_t s);
+hipError_t sst_emit(const SstArgs& a, hipStream_t s);
+hipError_t sst_scan(const uint32_t* counts, uint64_t* ebase, uint64_t nblocks, void* tmp, size_t* tmp_bytes,
+                    hipStream_t s);
+hipError_t gen_sst_fixed(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* data, uint32_t* blocks,
+                         hipStream_t s);
 }  // namespace vbf

@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     const bool own = (pl.G == 1) && !atomic_merge;  // sole writer: start from the existing words
     for (uint32_t w = tid * 4; w < kSegWords; w += kPBlock * 4) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (own) {
+        if (own && pl.ablate < 6) {
             if (w + 4 <= wn)
                 v = *reinterpret_cast<const uint4*>(words + wbase + w);
             else if (w < wn) {
@@ -293,6 +293,7 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     }
     __syncthreads();
 
+    if (pl.ablate < 5) {  // 5-7: timing experiments, fixed costs only
     const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / pl.G);
     const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / pl.G);
     const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
@@ -356,7 +357,9 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
         }
         tg = tn;
     }
+    }
     __syncthreads();
+    if (pl.ablate == 7) return;
     if (own) {
         for (uint32_t w = tid * 4; w < wn; w += kPBlock * 4) {
             if (w + 4 <= wn)

@@ -182,6 +182,46 @@ class BloomFilter:
         except VbfError as e:
             _raise("contains", e)
 
+    # -- SST rebuild (range.rs:117-128) ---------------------------------------------------
+    def rebuild_from_sst(self, data, index):
+        """load_entries_from_file + build_filter_from_entries (range.rs:124-125) in one device
+        pass: decode data.db (bytes) with its index.db (bytes) and OR every key into the bits.
+        Returns the number of entries (no_of_elements grows by it, as bf.rs:90 does per key)."""
+        a = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else \
+            np.ascontiguousarray(data, dtype=np.uint8)
+        b = np.frombuffer(index, dtype=np.uint8) if isinstance(index, (bytes, bytearray)) else \
+            np.ascontiguousarray(index, dtype=np.uint8)
+        n = ctypes.c_uint64()
+        try:
+            call("vbf_filter_rebuild_from_sst_host", self._h, a.ctypes.data if a.size else None, a.size,
+                 b.ctypes.data if b.size else None, b.size, ctypes.byref(n))
+        except VbfError as e:
+            _raise("rebuild", e)
+        return n.value
+
+    def rebuild_from_sst_dev(self, data_ptr, length, blocks_ptr, nblocks, stream=None):
+        """Device-resident data.db bytes and block offsets (u32)."""
+        n = ctypes.c_uint64()
+        try:
+            call("vbf_filter_rebuild_from_sst_dev", self._h, data_ptr, length, blocks_ptr, nblocks,
+                 ctypes.byref(n), stream)
+        except VbfError as e:
+            _raise("rebuild", e)
+        return n.value
+
+    def recover_from_sst_dir(self, sst_dir):
+        """The lazy recovery of range.rs:117-128 for one SST directory: recover_meta() from its
+        filter.db, then -- unless persisted bits were restored (filter_file.py) -- rebuild from
+        data.db + index.db.  Returns True when the bits came from filter.db."""
+        from . import sst
+        self.file_path = os.path.join(os.fspath(sst_dir), FILTER_FILE_NAME + ".db")
+        if self.recover_meta():
+            self.sst_dir = os.fspath(sst_dir)
+            return True
+        self.sst_dir = os.fspath(sst_dir)
+        self.rebuild_from_sst(*sst.read_sst_files(sst_dir))
+        return False
+
     # -- bits ----------------------------------------------------------------------------
     def words(self):
         """The bit array as uint32 words (bit-vec BitVec<u32> storage)."""
