@@ -24,6 +24,7 @@
  *   DataFileNode::load_entries         src/fs/mod.rs:275-332       -> vbf_sst_decode_dev / _host
  *   index.db block offsets             src/index/indexer.rs:151-170 -> vbf_sst_index_blocks
  *   lazy filter rebuild                src/key_range/range.rs:117-128 -> vbf_filter_rebuild_from_sst_*
+ *   KeyRange::filter_sstables_by_key_range src/key_range/range.rs:91-147 -> vbf_multi_probe_* (batch)
  *
  * Key batches.  `keys` holds the key bytes back to back.  When `offsets` is non-NULL it has
  * n+1 nondecreasing entries and key j is keys[offsets[j] .. offsets[j+1]) (positions are
@@ -208,6 +209,22 @@ int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t
                                     void* stream);
 int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_t len,
                                      const uint8_t* index, uint64_t index_len, uint64_t* n_out);
+
+/* ---- batched read-path probe across SSTs ----
+ * For n keys and nsst filters: out[j * nsst + s] = 1 iff SST s is a candidate for key j, i.e.
+ * the key lies in [smallest_s, biggest_s] (Vec<u8> order; skipped when bounds_off is NULL) and
+ * filters[s]->contains(key) -- the test KeyRange::filter_sstables_by_key_range applies per key
+ * (src/key_range/range.rs:118,136).  Each key is hashed once for all filters.
+ * filters: host array of handles, all on one device.  bounds / bounds_off (host): smallest_s =
+ * bounds[bounds_off[2s] .. bounds_off[2s+1]), biggest_s = bounds[bounds_off[2s+1] ..
+ * bounds_off[2s+2]).  A filter with m == 0 and k > 0 is VBF_EDIVZERO (bf.rs:100).
+ * _dev: keys / offsets / out on that device, queued on `stream`.  _host: host buffers, synchronous. */
+int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                        int len_prefix, uint32_t nsst, const vbf_filter* const* filters,
+                        const uint8_t* bounds, const uint64_t* bounds_off, uint8_t* out, void* stream);
+int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                         int len_prefix, uint32_t nsst, const vbf_filter* const* filters,
+                         const uint8_t* bounds, const uint64_t* bounds_off, uint8_t* out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,108 @@
+"""GPU parity for the batched read-path probe across SSTs:
+out[j, s] = smallest_s <= key_j <= biggest_s && filter_s.contains(key_j) (range.rs:118,136),
+checked against the oracle's probe (bf.rs:95-105) and Python's bytes order (= Rust Ord for
+Vec<u8>).  Bit-exact."""
+import ctypes
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+SST = os.path.join(GOLDEN, "sst_fixtures")
+
+
+def _oracle_contains(ora, keys, m, k, words):
+    from velarixdb_amd.keys import pack
+    return ora.probe(pack(keys), m, k, words).astype(bool)
+
+
+def test_fixture_ssts_candidates(vbf, ora):
+    from velarixdb_amd.key_range import SstRange, candidates, filter_sstables_many
+    ranges, all_keys, orc = [], [], []
+    for name in sorted(os.listdir(SST)):
+        data, index = vbf.sst.read_sst_files(os.path.join(SST, name))
+        ent = vbf.sst.load_entries(data, index)
+        keys = ent.key_list()
+        bf = vbf.BloomFilter.default()
+        bf.file_path = os.path.join(SST, name, "filter.db")
+        bf.recover_meta(load_bits=False)
+        bf.rebuild_from_sst(data, index)
+        ranges.append(SstRange(keys[0], keys[-1], bf))
+        words = ora.build_words(vbf.pack(keys), bf.num_bits(), bf.no_of_hash_func)
+        orc.append((keys[0], keys[-1], bf.num_bits(), bf.no_of_hash_func, words))
+        all_keys += keys[::7]
+    q = all_keys + [b"", b"0", b"zzzzzz", b"head", b"00", b"\xff" * 9] + \
+        [r.smallest_key for r in ranges] + [r.biggest_key for r in ranges] + \
+        [r.smallest_key[:-1] for r in ranges] + [r.biggest_key + b"\0" for r in ranges] + \
+        [b"k%06d" % i for i in range(3000)]
+    got = candidates(q, ranges)
+    want = np.zeros_like(got)
+    for s, (lo, hi, m, k, words) in enumerate(orc):
+        inr = np.array([lo <= x <= hi for x in q])
+        want[:, s] = inr & _oracle_contains(ora, q, m, k, words)
+    assert np.array_equal(got, want)
+    assert got[: len(all_keys)].any(axis=1).all()  # every stored key finds its SST
+    lists = filter_sstables_many(q[:50], ranges)
+    assert lists == [np.flatnonzero(r).tolist() for r in want[:50]]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_random_filters_contains_all(vbf, ora, seed):
+    from velarixdb_amd.key_range import contains_all
+    rng = np.random.default_rng(seed)
+    specs = [(0.01, 50), (0.1, 1000), (1e-4, 300), (0.5, 3), (1.0, 5), (0.3, 20000), (1e-7, 64)]
+    filters, orc = [], []
+    for p, n in specs:
+        f = vbf.BloomFilter(p, n)
+        ks = [rng.bytes(int(rng.integers(0, 40))) for _ in range(n)]
+        f.set_many(ks)
+        filters.append(f)
+        orc.append((f.num_bits(), f.no_of_hash_func, ora.build_words(vbf.pack(ks), f.num_bits(), f.no_of_hash_func)))
+    q = [rng.bytes(int(rng.integers(0, 70))) for _ in range(20000)]
+    got = contains_all(q, filters)
+    for s, (m, k, words) in enumerate(orc):
+        assert np.array_equal(got[:, s], _oracle_contains(ora, q, m, k, words)), s
+    assert got[:, 4].all()  # p = 1.0 -> m = 0, k = 0: contains() is vacuously true
+
+
+def test_device_api_matches_single_probes(vbf):
+    """2M device-resident fixed keys x 8 filters: vbf_multi_probe_dev equals 8 single probes."""
+    import torch
+    from velarixdb_amd._lib import call
+    n, L, S = 2_000_000, 16, 8
+    dev = torch.device("cuda:0")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    keys = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    call("vbf_gen_fixed_dev", 0x5EED0001, 0, n, L, P(keys), None)
+    filters = []
+    for s in range(S):
+        f = vbf.BloomFilter(0.01 * (s + 1) / 4, n // (s + 1))
+        f.set_dev(P(keys[s * 1000 * L:]), None, L, n // (s + 1) - s * 1000 if s else n // (s + 1), 1)
+        filters.append(f)
+    out = torch.empty(n * S, dtype=torch.uint8, device=dev)
+    handles = (ctypes.c_void_p * S)(*[f._h.value for f in filters])
+    call("vbf_multi_probe_dev", P(keys), None, L, n, 1, S, handles, None, None, P(out), None)
+    torch.cuda.synchronize()
+    got = out.view(n, S).cpu().numpy()
+    for s, f in enumerate(filters):
+        one = torch.empty(n, dtype=torch.uint8, device=dev)
+        f.contains_dev(P(keys), None, L, n, P(one))
+        torch.cuda.synchronize()
+        assert np.array_equal(got[:, s], one.cpu().numpy()), s
+
+
+def test_zero_bits_with_hashes_raises(vbf):
+    from velarixdb_amd.key_range import contains_all
+    from velarixdb_amd._lib import call
+    h = ctypes.c_void_p()
+    meta = (ctypes.c_uint8 * 16).from_buffer_copy(struct.pack("<IId", 3, 10, 1.0))  # m = 0, k = 3
+    call("vbf_filter_recover", meta, 16, 0, ctypes.byref(h))
+    bad = vbf.BloomFilter(_handle=h)
+    assert bad.num_bits() == 0 and bad.no_of_hash_func == 3
+    with pytest.raises(ZeroDivisionError):
+        contains_all([b"a"], [vbf.BloomFilter(0.01, 10), bad])
+    assert contains_all([], [bad]).shape == (0, 1)

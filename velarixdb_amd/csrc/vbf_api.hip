@@ -97,7 +97,7 @@ vbf::KeyBatch batch(const uint8_t* keys, const uint64_t* offsets, uint64_t off_b
 // Partitioned-build workspace: one grow-only buffer per (device, stream), so concurrent
 // builds on different streams never share scratch.
 // ---------------------------------------------------------------------------------------
-enum WsSlot { kWsBuild = 0, kWsSstScratch = 1, kWsSstKeys = 2, kWsSstInput = 3 };
+enum WsSlot { kWsBuild = 0, kWsSstScratch = 1, kWsSstKeys = 2, kWsSstInput = 3, kWsMulti = 4, kWsMultiKeys = 5 };
 struct Workspace {
     int device;
     hipStream_t stream;
@@ -1053,6 +1053,136 @@ int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_
     if (blk.size()) HIP_TRY(hipMemcpyAsync(d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
     if ((rc = vbf_filter_rebuild_from_sst_dev(f, d_data, len, d_blk, blk.size(), n_out, st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
+    return ok();
+}
+
+}  // extern "C"
+
+// ---- batched probe across SSTs ----
+
+namespace {
+// Locks every distinct storage of `filters` in address order (clones share one), so two
+// concurrent multi-probes over overlapping sets cannot deadlock.
+struct MultiLock {
+    std::vector<std::unique_lock<std::mutex>> locks;
+    explicit MultiLock(const vbf_filter* const* filters, uint32_t nsst) {
+        std::vector<Storage*> v;
+        for (uint32_t s = 0; s < nsst; ++s) v.push_back(filters[s]->bits.get());
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        for (Storage* st : v) locks.emplace_back(st->mu);
+    }
+};
+
+int multi_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
+                uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds, const uint64_t* bounds_off,
+                uint8_t* out, hipStream_t s) {
+    if (nsst && !filters) return fail(VBF_EINVAL, "filters is NULL");
+    for (uint32_t i = 0; i < nsst; ++i) {
+        if (!filters[i]) return fail(VBF_EINVAL, "filters[%u] is NULL", i);
+        if (filters[i]->bits->device != filters[0]->bits->device)
+            return fail(VBF_EINVAL, "filters[%u] lives on device %d, filters[0] on %d", i, filters[i]->bits->device,
+                        filters[0]->bits->device);
+        // bf.rs:100 divides by m: the reference panics once a key reaches such a filter
+        if (filters[i]->bits->m == 0 && filters[i]->k > 0 && n)
+            return fail(VBF_EDIVZERO, "filters[%u]: m == 0 with k = %u (bf.rs:100 divides by zero)", i, filters[i]->k);
+    }
+    if (bounds_off) {
+        for (uint32_t i = 0; i < 2 * nsst; ++i)
+            if (bounds_off[i + 1] < bounds_off[i]) return fail(VBF_EINVAL, "bounds_off not nondecreasing at %u", i);
+        if (bounds_off[2 * nsst] && !bounds) return fail(VBF_EINVAL, "bounds is NULL");
+    }
+    if (!n || !nsst) return VBF_OK;
+    if (!out) return fail(VBF_EINVAL, "out is NULL");
+    std::vector<vbf::MultiSst> tab(nsst);
+    for (uint32_t i = 0; i < nsst; ++i) {
+        const Storage& st = *filters[i]->bits;
+        tab[i] = vbf::MultiSst{st.d_words, st.m, st.m ? ~0ull / st.m : 0, filters[i]->k, 0, 0, 0, 0, 0};
+        if (bounds_off) {
+            tab[i].lo_beg = bounds_off[2 * i];
+            tab[i].lo_end = tab[i].hi_beg = bounds_off[2 * i + 1];
+            tab[i].hi_end = bounds_off[2 * i + 2];
+        }
+    }
+    const uint64_t nb = bounds_off ? bounds_off[2 * nsst] : 0;
+    const uint64_t o_b = align256(nsst * sizeof(vbf::MultiSst));
+    void* ws = nullptr;
+    int rc = get_workspace(s, o_b + nb + 8, &ws, kWsMulti);
+    if (rc) return rc;
+    // the table is read by this launch only; the stream orders reuse by the next call
+    HIP_TRY(hipMemcpyAsync(ws, tab.data(), nsst * sizeof(vbf::MultiSst), hipMemcpyHostToDevice, s));
+    uint8_t* d_bounds = nullptr;
+    if (bounds_off) {
+        d_bounds = static_cast<uint8_t*>(ws) + o_b;
+        if (nb) HIP_TRY(hipMemcpyAsync(d_bounds, bounds, nb, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));  // pageable sources: keep them alive only for this call
+    vbf::MultiArgs a{keys, offsets, 0, stride, n, nsst,
+                     static_cast<const vbf::MultiSst*>(ws), d_bounds, out};
+    HIP_TRY(vbf::launch_multi_probe(a, len_prefix != 0, s));
+    return VBF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
+                        uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
+                        const uint64_t* bounds_off, uint8_t* out, void* stream) {
+    int rc = check_keys(keys, offsets, stride, n);
+    if (rc) return rc;
+    if (nsst && filters && filters[0]) {
+        DEVICE_SCOPE(filters[0]->bits->device);
+        MultiLock lk(filters, nsst);
+        if ((rc = multi_probe(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out,
+                              (hipStream_t)stream)))
+            return rc;
+        return ok();
+    }
+    if ((rc = multi_probe(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out,
+                          (hipStream_t)stream)))
+        return rc;
+    return ok();
+}
+
+int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
+                         uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
+                         const uint64_t* bounds_off, uint8_t* out) {
+    int rc = check_keys(keys, offsets, stride, n);
+    if (rc) return rc;
+    if (!nsst || !n) {
+        if ((rc = multi_probe(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out, nullptr)))
+            return rc;
+        return ok();
+    }
+    if (!filters || !filters[0]) return fail(VBF_EINVAL, "filters is NULL");
+    if (!out) return fail(VBF_EINVAL, "out is NULL");
+    DEVICE_SCOPE(filters[0]->bits->device);
+    hipStream_t s;
+    if ((rc = filter_stream(filters[0]->bits->device, &s))) return rc;
+    const uint64_t kbytes = offsets ? offsets[n] - offsets[0] : n * stride;
+    const uint64_t o_off = align256(kbytes), o_out = o_off + align256(offsets ? (n + 1) * 8 : 0);
+    void* ws = nullptr;
+    if ((rc = get_workspace(s, o_out + n * nsst, &ws, kWsMultiKeys))) return rc;
+    uint8_t* d_keys = static_cast<uint8_t*>(ws);
+    uint64_t* d_off = offsets ? reinterpret_cast<uint64_t*>(d_keys + o_off) : nullptr;
+    uint8_t* d_out = d_keys + o_out;
+    if (kbytes) HIP_TRY(hipMemcpyAsync(d_keys, keys + (offsets ? offsets[0] : 0), kbytes, hipMemcpyHostToDevice, s));
+    if (offsets) {
+        // rebase to absolute positions in the device copy
+        std::vector<uint64_t> o(offsets, offsets + n + 1);
+        const uint64_t b0 = o[0];
+        for (auto& x : o) x -= b0;
+        HIP_TRY(hipMemcpyAsync(d_off, o.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    {
+        MultiLock lk(filters, nsst);
+        if ((rc = multi_probe(d_keys, d_off, stride, n, len_prefix, nsst, filters, bounds, bounds_off, d_out, s)))
+            return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(out, d_out, n * nsst, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
     return ok();
 }
 

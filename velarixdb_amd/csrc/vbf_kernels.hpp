@@ -65,6 +65,23 @@ hipError_t sst_count(const SstArgs& a, hipStream_t s);
 hipError_t sst_emit(const SstArgs& a, hipStream_t s);
 hipError_t sst_scan(const uint32_t* counts, uint64_t* ebase, uint64_t nblocks, void* tmp, size_t* tmp_bytes,
                     hipStream_t s);
+// Batched probe across SSTs (vbf_multi.hip).
+struct MultiSst {
+    const uint32_t* words;
+    uint64_t m, mu;
+    uint32_t k, pad;
+    uint64_t lo_beg, lo_end, hi_beg, hi_end;  // smallest / biggest key in `bounds`
+};
+struct MultiArgs {
+    const uint8_t* keys;
+    const uint64_t* offsets;
+    uint64_t off_base, stride, n;
+    uint32_t nsst;
+    const MultiSst* tab;    // device table, nsst entries
+    const uint8_t* bounds;  // device, NULL = no key-range test
+    uint8_t* out;           // n * nsst
+};
+hipError_t launch_multi_probe(const MultiArgs& a, bool len_prefix, hipStream_t s);
 hipError_t gen_sst_fixed(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* data, uint32_t* blocks,
                          hipStream_t s);
 }  // namespace vbf

@@ -1,0 +1,92 @@
+// Batched read-path probe across SSTs.
+//
+// velarixdb answers a get by walking its key ranges: an SST is a candidate when the key lies in
+// [smallest_key, biggest_key] (Vec<u8> order) and its filter contains the key
+// (KeyRange::filter_sstables_by_key_range, src/key_range/range.rs:91-147; filter.contains at
+// :136).  Per key and per SST it re-hashes the key k times (bf.rs:95-105).  Here one lane takes
+// one key against every SST: the seed-independent SipHash blocks are absorbed once, and since
+// calculate_hash(key, i) does not depend on the filter, the first four seed hashes are computed
+// once and reused by every SST (only `% m` and the bit test differ).
+//
+// Output: out[j * nsst + s] = 1 when SST s is a candidate for key j (bit-identical to the
+// reference's range test && contains()).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "keyhash.hpp"
+#include "sip13.hpp"
+#include "vbf_kernels.hpp"
+
+namespace vbf {
+
+// Rust `Ord for [u8]`: lexicographic, a proper prefix is smaller.  -1 / 0 / 1.
+__device__ __forceinline__ int cmp_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
+    const uint64_t n = la < lb ? la : lb;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t x = a[i], y = b[i];
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+template <int FMT, bool LP>
+__global__ __launch_bounds__(256) void k_multi_probe(MultiArgs a) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= a.n) return;
+    const DevKeys dk{a.keys, a.offsets, a.off_base, a.stride, a.n};
+    const uint8_t* kp;
+    uint64_t kl;
+    if (a.offsets) {
+        kp = a.keys + (a.offsets[j] - a.off_base);
+        kl = a.offsets[j + 1] - a.offsets[j];
+    } else {
+        kp = a.keys + j * a.stride;
+        kl = a.stride;
+    }
+    const Prefix p = key_prefix<FMT, LP>(dk, j);
+    uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    uint32_t have = 0;
+    auto hash = [&](uint32_t i) -> uint64_t {
+        if (i >= 4) return prefix_hash(p, i);
+        if (!((have >> i) & 1u)) {
+            const uint64_t v = prefix_hash(p, i);
+            if (i == 0) h0 = v;
+            else if (i == 1) h1 = v;
+            else if (i == 2) h2 = v;
+            else h3 = v;
+            have |= 1u << i;
+        }
+        return i == 0 ? h0 : i == 1 ? h1 : i == 2 ? h2 : h3;
+    };
+    uint8_t* out = a.out + j * a.nsst;
+    for (uint32_t s = 0; s < a.nsst; ++s) {
+        const MultiSst d = a.tab[s];
+        bool hit = true;
+        if (a.bounds) {  // range.rs:118: searched_key >= smallest_key && searched_key <= biggest_key
+            hit = cmp_bytes(kp, kl, a.bounds + d.lo_beg, d.lo_end - d.lo_beg) >= 0 &&
+                  cmp_bytes(kp, kl, a.bounds + d.hi_beg, d.hi_end - d.hi_beg) <= 0;
+        }
+        if (hit) {  // bf.rs:95-105, k == 0 -> true
+            for (uint32_t i = 0; i < d.k; ++i) {
+                const uint32_t idx = fast_mod(hash(i), d.m, d.mu);
+                if (!((d.words[idx >> 5] >> (idx & 31)) & 1u)) {
+                    hit = false;
+                    break;
+                }
+            }
+        }
+        out[s] = hit ? 1 : 0;
+    }
+}
+
+hipError_t launch_multi_probe(const MultiArgs& a, bool len_prefix, hipStream_t s) {
+    if (a.n == 0 || a.nsst == 0) return hipSuccess;
+    const uint64_t blocks = (a.n + 255) / 256;
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    with_fmt(pick_fmt(a.keys, a.offsets, a.stride), len_prefix, [&]<int FMT, bool LP>() {
+        hipLaunchKernelGGL((k_multi_probe<FMT, LP>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    });
+    return hipGetLastError();
+}
+
+}  // namespace vbf
