@@ -25,6 +25,7 @@
  *   index.db block offsets             src/index/indexer.rs:151-170 -> vbf_sst_index_blocks
  *   lazy filter rebuild                src/key_range/range.rs:117-128 -> vbf_filter_rebuild_from_sst_*
  *   KeyRange::filter_sstables_by_key_range src/key_range/range.rs:91-147 -> vbf_multi_probe_* (batch)
+ *   SizedTierRunner::merge_ssts_in_buckets src/compactors/sized.rs:170-320 -> vbf_compact_merge_*
  *
  * Key batches.  `keys` holds the key bytes back to back.  When `offsets` is non-NULL it has
  * n+1 nondecreasing entries and key j is keys[offsets[j] .. offsets[j+1]) (positions are
@@ -225,6 +226,42 @@ int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t s
 int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                          int len_prefix, uint32_t nsst, const vbf_filter* const* filters,
                          const uint8_t* bounds, const uint64_t* bounds_off, uint8_t* out);
+
+/* ---- compaction merge ----
+ * One bucket of SizedTierRunner::merge_ssts_in_buckets (src/compactors/sized.rs:170-200): the
+ * pairwise fold merged = tables[0], merged = merge_sstables(merged, t) (:207-283) with
+ * tombstone_check (:286-320) at every pairwise merge.  Input: an arena of all tables' entries,
+ * table r = entries run_off[r] .. run_off[r+1] (host array, run_off[0] = 0), each table strictly
+ * increasing by key (a SkipMap; VBF_EINVAL otherwise); entry e = keys[offsets[e] ..
+ * offsets[e+1]), created_ms[e] (i64 ms), tombstones[e] (0/1).  The compactor's tombstone map
+ * enters as sorted unique keys (map_keys/map_off, map_n + 1 offsets) with times map_time;
+ * map_n = 0 for an empty map.  TTLs as Config (use_ttl, entry_ttl, tombstone_ttl in ms) and
+ * `now_ms` for Entry::has_expired (memtable/mem.rs:149-153: now > created + ttl).
+ * Output: the merged table's entry ids in key order (out_ids, capacity = all entries), *n_out;
+ * and, when upd_ids/upd_time are non-NULL, the keys whose map value changed (an entry id holding
+ * the key) with their new time, *n_upd (capacity = all entries).  Synchronous on the stream. */
+int vbf_compact_merge_dev(const uint8_t* keys, const uint64_t* offsets, const int64_t* created_ms,
+                          const uint8_t* tombstones, const uint64_t* run_off, uint32_t nruns,
+                          const uint8_t* map_keys, const uint64_t* map_off, const int64_t* map_time,
+                          uint64_t map_n, int use_ttl, uint64_t entry_ttl_ms, uint64_t tombstone_ttl_ms,
+                          uint64_t now_ms, uint32_t* out_ids, uint64_t* n_out, uint32_t* upd_ids,
+                          int64_t* upd_time, uint64_t* n_upd, void* stream);
+/* Same with every array in host memory, merged on `device`. */
+int vbf_compact_merge_host(const uint8_t* keys, const uint64_t* offsets, const int64_t* created_ms,
+                           const uint8_t* tombstones, const uint64_t* run_off, uint32_t nruns,
+                           const uint8_t* map_keys, const uint64_t* map_off, const int64_t* map_time,
+                           uint64_t map_n, int use_ttl, uint64_t entry_ttl_ms,
+                           uint64_t tombstone_ttl_ms, uint64_t now_ms, uint32_t* out_ids,
+                           uint64_t* n_out, uint32_t* upd_ids, int64_t* upd_time, uint64_t* n_upd,
+                           int device);
+/* ids -> the build's key layout: out_keys packed (capacity out_keys_cap), out_offsets n+1 (from 0),
+ * and optionally the per-entry arrays (each needs its input).  *key_bytes (may be NULL) = packed
+ * size.  Device pointers; one readback of the size. */
+int vbf_gather_entries_dev(const uint8_t* keys, const uint64_t* offsets, const int64_t* created_ms,
+                           const uint8_t* tombstones, const uint32_t* val_offsets, const uint32_t* ids,
+                           uint64_t n, uint8_t* out_keys, uint64_t out_keys_cap, uint64_t* out_offsets,
+                           int64_t* out_created_ms, uint8_t* out_tombstones, uint32_t* out_val_offsets,
+                           uint64_t* key_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -56,6 +56,20 @@ def _load():
     L.ora_sst_decode.argtypes = [vp, u64, vp, vp, vp, vp, vp]
     L.ora_sst_index_blocks.restype = ctypes.c_int64
     L.ora_sst_index_blocks.argtypes = [vp, u64, vp]
+    L.ora_tmap_new.restype = vp
+    L.ora_tmap_new.argtypes = []
+    L.ora_tmap_free.restype = None
+    L.ora_tmap_free.argtypes = [vp]
+    L.ora_tmap_set.restype = None
+    L.ora_tmap_set.argtypes = [vp, vp, u64, ctypes.c_int64]
+    L.ora_tmap_get.restype = i
+    L.ora_tmap_get.argtypes = [vp, vp, u64, vp]
+    L.ora_tmap_size.restype = u64
+    L.ora_tmap_size.argtypes = [vp]
+    L.ora_tmap_dump.restype = u64
+    L.ora_tmap_dump.argtypes = [vp, vp, vp, vp]
+    L.ora_compact_merge.restype = ctypes.c_int64
+    L.ora_compact_merge.argtypes = [vp, vp, vp, vp, vp, u32, i, u64, u64, u64, vp, vp]
     return L
 
 
@@ -180,3 +194,56 @@ def sst_index_blocks(index):
     offs = np.zeros(nb, dtype=np.uint32)
     lib.ora_sst_index_blocks(_p(index), index.size, _p(offs))
     return offs
+
+
+class TombstoneMap:
+    """The compactor's `tombstones: HashMap<Key, CreatedAt>` (compactors/sized.rs:36)."""
+
+    def __init__(self, items=None):
+        self.h = lib.ora_tmap_new()
+        for k, t in (items or {}).items():
+            self[k] = t
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib.ora_tmap_free(self.h)
+            self.h = None
+
+    def __setitem__(self, key, t):
+        lib.ora_tmap_set(self.h, key, len(key), int(t))
+
+    def get(self, key):
+        t = ctypes.c_int64()
+        return t.value if lib.ora_tmap_get(self.h, key, len(key), ctypes.byref(t)) else None
+
+    def __len__(self):
+        return lib.ora_tmap_size(self.h)
+
+    def items(self):
+        n = len(self)
+        lens = np.zeros(n, np.uint64)
+        times = np.zeros(n, np.int64)
+        kb = lib.ora_tmap_dump(self.h, None, None, None)
+        keys = np.zeros(max(kb, 1), np.uint8)
+        lib.ora_tmap_dump(self.h, keys.ctypes.data, _p(lens), _p(times))
+        out, o = {}, 0
+        for L, t in zip(lens.tolist(), times.tolist()):
+            out[keys[o:o + L].tobytes()] = t
+            o += L
+        return out
+
+
+def compact_merge(keys, offsets, created, tomb, run_off, use_ttl=False, entry_ttl_ms=0,
+                  tomb_ttl_ms=0, now_ms=0, tmap=None):
+    """One bucket through merge_ssts_in_buckets' fold (sized.rs:170-320) -> merged entry ids."""
+    keys = np.ascontiguousarray(keys, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    created = np.ascontiguousarray(created, np.int64)
+    tomb = np.ascontiguousarray(tomb, np.uint8)
+    run_off = np.ascontiguousarray(run_off, np.uint64)
+    tmap = tmap if tmap is not None else TombstoneMap()
+    out = np.zeros(max(int(run_off[-1]), 1), np.uint32)
+    n = lib.ora_compact_merge(_p(keys), offsets.ctypes.data, _p(created), _p(tomb), run_off.ctypes.data,
+                              run_off.size - 1, int(use_ttl), entry_ttl_ms, tomb_ttl_ms, now_ms, tmap.h,
+                              out.ctypes.data)
+    return out[:n]

@@ -406,3 +406,203 @@ int64_t ora_sst_index_blocks(const uint8_t* index, uint64_t len, uint32_t* offs)
     }
     return nb;
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * Compaction merge: SizedTierRunner::merge_ssts_in_buckets folds a
+ * bucket's tables pairwise -- merged = tables[0]; merged = merge_sstables(merged, t) for the
+ * rest (compactors/sized.rs:170-200) -- and every pairwise merge passes each surviving entry
+ * through tombstone_check (:286-320), whose `tombstones` map lives across merges and buckets
+ * (cleared only when compaction finds nothing left to do, :73-75).  Restated literally here.
+ * ------------------------------------------------------------------------------------------- */
+
+typedef struct {
+    uint8_t** keys;
+    uint64_t* lens;
+    int64_t* times;
+    uint8_t* used;
+    uint64_t cap, size;
+} ora_tmap;
+
+static uint64_t fnv(const uint8_t* k, uint64_t n) {
+    uint64_t h = 1469598103934665603ULL;
+    for (uint64_t i = 0; i < n; ++i) h = (h ^ k[i]) * 1099511628211ULL;
+    return h;
+}
+
+void* ora_tmap_new(void) {
+    ora_tmap* m = (ora_tmap*)calloc(1, sizeof(ora_tmap));
+    m->cap = 1024;
+    m->keys = (uint8_t**)calloc(m->cap, sizeof(uint8_t*));
+    m->lens = (uint64_t*)calloc(m->cap, sizeof(uint64_t));
+    m->times = (int64_t*)calloc(m->cap, sizeof(int64_t));
+    m->used = (uint8_t*)calloc(m->cap, 1);
+    return m;
+}
+
+void ora_tmap_free(void* p) {
+    ora_tmap* m = (ora_tmap*)p;
+    if (!m) return;
+    for (uint64_t i = 0; i < m->cap; ++i) free(m->keys[i]);
+    free(m->keys);
+    free(m->lens);
+    free(m->times);
+    free(m->used);
+    free(m);
+}
+
+static uint64_t tmap_slot(const ora_tmap* m, const uint8_t* k, uint64_t n) {
+    uint64_t i = fnv(k, n) & (m->cap - 1);
+    while (m->used[i] && !(m->lens[i] == n && (n == 0 || memcmp(m->keys[i], k, n) == 0))) i = (i + 1) & (m->cap - 1);
+    return i;
+}
+
+int ora_tmap_get(void* p, const uint8_t* k, uint64_t n, int64_t* t) {
+    ora_tmap* m = (ora_tmap*)p;
+    uint64_t i = tmap_slot(m, k, n);
+    if (!m->used[i]) return 0;
+    *t = m->times[i];
+    return 1;
+}
+
+void ora_tmap_set(void* p, const uint8_t* k, uint64_t n, int64_t t) {
+    ora_tmap* m = (ora_tmap*)p;
+    if (2 * (m->size + 1) > m->cap) { /* grow */
+        ora_tmap old = *m;
+        m->cap *= 2;
+        m->keys = (uint8_t**)calloc(m->cap, sizeof(uint8_t*));
+        m->lens = (uint64_t*)calloc(m->cap, sizeof(uint64_t));
+        m->times = (int64_t*)calloc(m->cap, sizeof(int64_t));
+        m->used = (uint8_t*)calloc(m->cap, 1);
+        for (uint64_t i = 0; i < old.cap; ++i)
+            if (old.used[i]) {
+                uint64_t j = tmap_slot(m, old.keys[i], old.lens[i]);
+                m->used[j] = 1;
+                m->keys[j] = old.keys[i];
+                m->lens[j] = old.lens[i];
+                m->times[j] = old.times[i];
+            }
+        free(old.keys);
+        free(old.lens);
+        free(old.times);
+        free(old.used);
+    }
+    uint64_t i = tmap_slot(m, k, n);
+    if (!m->used[i]) {
+        m->used[i] = 1;
+        m->keys[i] = (uint8_t*)malloc(n ? n : 1);
+        if (n) memcpy(m->keys[i], k, n);
+        m->lens[i] = n;
+        m->size++;
+    }
+    m->times[i] = t;
+}
+
+uint64_t ora_tmap_size(void* p) { return ((ora_tmap*)p)->size; }
+
+/* Dump the map: keys into `keys` (NULL to size), lens, times; returns total key bytes. */
+uint64_t ora_tmap_dump(void* p, uint8_t* keys, uint64_t* lens, int64_t* times) {
+    ora_tmap* m = (ora_tmap*)p;
+    uint64_t kb = 0, j = 0;
+    for (uint64_t i = 0; i < m->cap; ++i)
+        if (m->used[i]) {
+            if (keys) memcpy(keys + kb, m->keys[i], m->lens[i]);
+            if (lens) lens[j] = m->lens[i];
+            if (times) times[j] = m->times[i];
+            kb += m->lens[i];
+            ++j;
+        }
+    return kb;
+}
+
+typedef struct {
+    const uint8_t* keys;
+    const uint64_t* offsets;
+    const int64_t* created;
+    const uint8_t* tomb;
+    int use_ttl;
+    uint64_t entry_ttl, tomb_ttl, now;
+    ora_tmap* map;
+} merge_ctx;
+
+static int key_cmp(const merge_ctx* c, uint32_t a, uint32_t b) {
+    const uint64_t la = c->offsets[a + 1] - c->offsets[a], lb = c->offsets[b + 1] - c->offsets[b];
+    const uint64_t n = la < lb ? la : lb;
+    int r = n ? memcmp(c->keys + c->offsets[a], c->keys + c->offsets[b], n) : 0;
+    if (r) return r < 0 ? -1 : 1;
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+/* Entry::has_expired (memtable/mem.rs:149-153): now > created + ttl, in u64 ms. */
+static int expired(const merge_ctx* c, uint32_t e, uint64_t ttl) {
+    return c->now > (uint64_t)c->created[e] + ttl;
+}
+
+/* tombstone_check (sized.rs:291-320). */
+static void tomb_check(merge_ctx* c, uint32_t e, uint32_t* out, uint64_t* n_out) {
+    const uint8_t* k = c->keys + c->offsets[e];
+    const uint64_t n = c->offsets[e + 1] - c->offsets[e];
+    int ins = 0;
+    int64_t t;
+    if (ora_tmap_get(c->map, k, n, &t)) {
+        if (c->created[e] > t) {
+            if (c->tomb[e]) {
+                ora_tmap_set(c->map, k, n, c->created[e]);
+                ins = !expired(c, e, c->tomb_ttl);
+            } else if (c->use_ttl) {
+                ins = !expired(c, e, c->entry_ttl);
+            } else {
+                ins = 1;
+            }
+        }
+    } else if (c->tomb[e]) {
+        ora_tmap_set(c->map, k, n, c->created[e]);
+        ins = !expired(c, e, c->tomb_ttl);
+    } else if (c->use_ttl) {
+        ins = !expired(c, e, c->entry_ttl);
+    } else {
+        ins = 1;
+    }
+    if (ins) out[(*n_out)++] = e;
+}
+
+/* One bucket: entries of table t are ids run_off[t] .. run_off[t+1] (each table sorted by key,
+ * unique -- a SkipMap).  Writes the merged table's entry ids in key order to out_ids and returns
+ * their count; `tmap` carries the tombstone map in and out. */
+int64_t ora_compact_merge(const uint8_t* keys, const uint64_t* offsets, const int64_t* created,
+                          const uint8_t* tomb, const uint64_t* run_off, uint32_t nruns, int use_ttl,
+                          uint64_t entry_ttl_ms, uint64_t tomb_ttl_ms, uint64_t now_ms, void* tmap,
+                          uint32_t* out_ids) {
+    merge_ctx c = {keys, offsets, created, tomb, use_ttl, entry_ttl_ms, tomb_ttl_ms, now_ms, (ora_tmap*)tmap};
+    if (nruns == 0) return 0;
+    const uint64_t total = run_off[nruns] - run_off[0];
+    uint32_t* cur = (uint32_t*)malloc((total + 1) * sizeof(uint32_t));
+    uint32_t* nxt = (uint32_t*)malloc((total + 1) * sizeof(uint32_t));
+    uint64_t ncur = 0;
+    for (uint64_t e = run_off[0]; e < run_off[1]; ++e) cur[ncur++] = (uint32_t)e; /* merged = tables[0] */
+    for (uint32_t t = 1; t < nruns; ++t) {                                        /* merge_sstables */
+        uint64_t p1 = 0, p2 = run_off[t], e2 = run_off[t + 1], nn = 0;
+        while (p1 < ncur && p2 < e2) {
+            const int r = key_cmp(&c, cur[p1], (uint32_t)p2);
+            if (r < 0) {
+                tomb_check(&c, cur[p1++], nxt, &nn);
+            } else if (r == 0) {
+                if (created[cur[p1]] > created[p2]) tomb_check(&c, cur[p1], nxt, &nn);
+                else tomb_check(&c, (uint32_t)p2, nxt, &nn);
+                ++p1;
+                ++p2;
+            } else {
+                tomb_check(&c, (uint32_t)p2++, nxt, &nn);
+            }
+        }
+        while (p1 < ncur) tomb_check(&c, cur[p1++], nxt, &nn);
+        while (p2 < e2) tomb_check(&c, (uint32_t)p2++, nxt, &nn);
+        uint32_t* sw = cur;
+        cur = nxt;
+        nxt = sw;
+        ncur = nn;
+    }
+    memcpy(out_ids, cur, ncur * sizeof(uint32_t));
+    free(cur);
+    free(nxt);
+    return (int64_t)ncur;
+}

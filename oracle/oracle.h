@@ -75,6 +75,19 @@ int64_t ora_sst_decode(const uint8_t* data, uint64_t len, uint8_t* keys, uint64_
                        uint32_t* val_off, uint64_t* created_ms, uint8_t* tomb);
 int64_t ora_sst_index_blocks(const uint8_t* index, uint64_t len, uint32_t* offs);
 
+/* Compaction merge: the pairwise fold of compactors/sized.rs:170-283 with
+ * tombstone_check (:286-320) and its persistent tombstone map (an opaque handle here). */
+void* ora_tmap_new(void);
+void ora_tmap_free(void* m);
+void ora_tmap_set(void* m, const uint8_t* key, uint64_t len, int64_t t);
+int ora_tmap_get(void* m, const uint8_t* key, uint64_t len, int64_t* t);
+uint64_t ora_tmap_size(void* m);
+uint64_t ora_tmap_dump(void* m, uint8_t* keys, uint64_t* lens, int64_t* times);
+int64_t ora_compact_merge(const uint8_t* keys, const uint64_t* offsets, const int64_t* created,
+                          const uint8_t* tomb, const uint64_t* run_off, uint32_t nruns, int use_ttl,
+                          uint64_t entry_ttl_ms, uint64_t tomb_ttl_ms, uint64_t now_ms, void* tmap,
+                          uint32_t* out_ids);
+
 #ifdef __cplusplus
 }
 #endif

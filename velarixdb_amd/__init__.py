@@ -8,6 +8,6 @@ from ._lib import LIB_PATH, VbfError, device_count, lib  # noqa: F401
 from .filter import (DEFAULT_FALSE_POSITIVE_RATE, FILTER_FILE_NAME, BloomFilter,  # noqa: F401
                      num_bits, num_hash_functions)
 from .keys import HostBatch, I32Vec, RawMessage, Usize, pack, pack_fixed, pack_offsets  # noqa: F401
-from . import key_range, sst  # noqa: F401
+from . import compaction, key_range, sst  # noqa: F401
 
 __version__ = "0.1.0"

@@ -76,6 +76,11 @@ SIGNATURES = {
     "vbf_gen_sst_fixed_dev": (_int, [_u64, _u64, _u64, _u32, _vp, _vp, _vp]),
     "vbf_multi_probe_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp, _vp, _vp, _vp]),
     "vbf_multi_probe_host": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp, _vp, _vp]),
+    "vbf_compact_merge_dev": (_int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _u64, _int, _u64, _u64, _u64,
+                                      _vp, _vp, _vp, _vp, _vp, _vp]),
+    "vbf_compact_merge_host": (_int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _u64, _int, _u64, _u64, _u64,
+                                       _vp, _vp, _vp, _vp, _vp, _int]),
+    "vbf_gather_entries_dev": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "vbf_sst_index_blocks": (_int, [_vp, _u64, _vp, _u64, _vp]),
     "vbf_sst_decode_dev": (_int, [_vp, _u64, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp, _vp]),
     "vbf_sst_decode_host": (_int, [_vp, _u64, _vp, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _u64, _vp, _int]),

@@ -97,7 +97,7 @@ vbf::KeyBatch batch(const uint8_t* keys, const uint64_t* offsets, uint64_t off_b
 // Partitioned-build workspace: one grow-only buffer per (device, stream), so concurrent
 // builds on different streams never share scratch.
 // ---------------------------------------------------------------------------------------
-enum WsSlot { kWsBuild = 0, kWsSstScratch = 1, kWsSstKeys = 2, kWsSstInput = 3, kWsMulti = 4, kWsMultiKeys = 5 };
+enum WsSlot { kWsBuild = 0, kWsSstScratch = 1, kWsSstKeys = 2, kWsSstInput = 3, kWsMulti = 4, kWsMultiKeys = 5, kWsCompact = 6, kWsCompactIn = 7, kWsGather = 8 };
 struct Workspace {
     int device;
     hipStream_t stream;
@@ -1183,6 +1183,205 @@ int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t 
     }
     HIP_TRY(hipMemcpyAsync(out, d_out, n * nsst, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    return ok();
+}
+
+}  // extern "C"
+
+// ---- compaction merge ----
+
+namespace {
+int compact_merge(const uint8_t* keys, const uint64_t* offsets, const int64_t* created, const uint8_t* tomb,
+                  const uint64_t* run_off, uint32_t nruns, const uint8_t* map_keys, const uint64_t* map_off,
+                  const int64_t* map_time, uint64_t map_n, int use_ttl, uint64_t entry_ttl_ms, uint64_t tomb_ttl_ms,
+                  uint64_t now_ms, uint32_t* out_ids, uint64_t* n_out, uint32_t* upd_ids, int64_t* upd_time,
+                  uint64_t* n_upd, hipStream_t s) {
+    if (!n_out) return fail(VBF_EINVAL, "n_out is NULL");
+    *n_out = 0;
+    if (n_upd) *n_upd = 0;
+    if (nruns == 0) return VBF_OK;
+    if (!run_off || run_off[0] != 0) return fail(VBF_EINVAL, "run_off must start at 0");
+    for (uint32_t r = 0; r < nruns; ++r)
+        if (run_off[r + 1] < run_off[r]) return fail(VBF_EINVAL, "run_off not nondecreasing at %u", r);
+    const uint64_t total = run_off[nruns];
+    if (total >= 0xFFFFFFFFull) return fail(VBF_EINVAL, "too many entries (%llu)", (unsigned long long)total);
+    if (total && (!keys && offsets == nullptr)) return fail(VBF_EINVAL, "keys/offsets are NULL");
+    if (total && (!offsets || !created || !tomb || !out_ids)) return fail(VBF_EINVAL, "NULL argument");
+    if (map_n && (!map_keys || !map_off || !map_time)) return fail(VBF_EINVAL, "map arrays are NULL");
+    if (total == 0) return VBF_OK;
+    // merge levels: segment boundaries per level, all uploaded at once
+    std::vector<uint64_t> bnd(run_off, run_off + nruns + 1);
+    std::vector<uint64_t> all;
+    std::vector<uint32_t> nseg_lv;
+    uint32_t nseg = nruns;
+    while (nseg > 1) {
+        all.insert(all.end(), bnd.begin(), bnd.end());
+        nseg_lv.push_back(nseg);
+        std::vector<uint64_t> nb;
+        for (uint32_t i = 0; i < nseg; i += 2) nb.push_back(bnd[i]);
+        nb.push_back(bnd[nseg]);
+        bnd.swap(nb);
+        nseg = (uint32_t)bnd.size() - 1;
+    }
+    size_t t1 = 0, t2 = 0, t3 = 0;
+    HIP_TRY(vbf::select_u32(nullptr, &t1, nullptr, nullptr, nullptr, nullptr, total, s));
+    HIP_TRY(vbf::select_i64(nullptr, &t2, nullptr, nullptr, nullptr, nullptr, total, s));
+    t3 = std::max(t1, t2);
+    const uint64_t o_pong = align256(total * 4), o_keep = o_pong + align256(total * 4);
+    const uint64_t o_sel = o_keep + align256(total), o_upd = o_sel + align256(total * 4);
+    const uint64_t o_ut = o_upd + align256(total), o_ro = o_ut + align256(total * 8);
+    const uint64_t o_bnd = o_ro + align256((nruns + 1) * 8), o_misc = o_bnd + align256(all.size() * 8 + 8);
+    const uint64_t o_tmp = o_misc + 256, bytes = o_tmp + t3;
+    void* ws = nullptr;
+    int rc = get_workspace(s, bytes, &ws, kWsCompact);
+    if (rc) return rc;
+    char* b = static_cast<char*>(ws);
+    uint32_t* ping = reinterpret_cast<uint32_t*>(b);
+    uint32_t* pong = reinterpret_cast<uint32_t*>(b + o_pong);
+    uint8_t* keep = reinterpret_cast<uint8_t*>(b + o_keep);
+    uint32_t* sel = reinterpret_cast<uint32_t*>(b + o_sel);
+    uint8_t* upd = reinterpret_cast<uint8_t*>(b + o_upd);
+    int64_t* ut = reinterpret_cast<int64_t*>(b + o_ut);
+    uint64_t* d_ro = reinterpret_cast<uint64_t*>(b + o_ro);
+    uint64_t* d_bnd = reinterpret_cast<uint64_t*>(b + o_bnd);
+    uint64_t* misc = reinterpret_cast<uint64_t*>(b + o_misc);  // [0] n_out, [1] n_upd, [2] sort error
+    HIP_TRY(hipMemcpyAsync(d_ro, run_off, (nruns + 1) * 8, hipMemcpyHostToDevice, s));
+    if (!all.empty()) HIP_TRY(hipMemcpyAsync(d_bnd, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(misc, 0, 16, s));
+    HIP_TRY(hipMemsetAsync(misc + 2, 0xFF, 8, s));
+    vbf::CompactArgs a{keys, offsets, created, tomb, d_ro, nruns, map_keys, map_off, map_time, map_n, use_ttl,
+                       entry_ttl_ms, tomb_ttl_ms, now_ms, total};
+    HIP_TRY(vbf::compact_check_sorted(a, reinterpret_cast<uint32_t*>(misc + 2), s));
+    HIP_TRY(vbf::launch_iota_u32(ping, total, s));
+    uint32_t* order = nullptr;
+    HIP_TRY(vbf::compact_merge_levels(a, d_bnd, nseg_lv.data(), (uint32_t)nseg_lv.size(), ping, pong, &order, s));
+    HIP_TRY(vbf::compact_fold(a, order, total, keep, sel, upd, ut, s));
+    size_t tb = t3;
+    HIP_TRY(vbf::select_u32(b + o_tmp, &tb, sel, keep, out_ids, misc, total, s));
+    if (upd_ids && upd_time) {
+        tb = t3;
+        HIP_TRY(vbf::select_u32(b + o_tmp, &tb, order, upd, upd_ids, misc + 1, total, s));
+        tb = t3;
+        HIP_TRY(vbf::select_i64(b + o_tmp, &tb, ut, upd, upd_time, misc + 1, total, s));
+    }
+    uint64_t hv[3];
+    HIP_TRY(hipMemcpyAsync(hv, misc, 24, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t bad = (uint32_t)hv[2];
+    if (bad != 0xFFFFFFFFu)
+        return fail(VBF_EINVAL, "run entries not strictly increasing at entry %u (tables are SkipMaps)", bad);
+    *n_out = hv[0];
+    if (n_upd) *n_upd = (upd_ids && upd_time) ? hv[1] : 0;
+    return VBF_OK;
+}
+
+int gather_entries(const uint8_t* keys, const uint64_t* offsets, const int64_t* created, const uint8_t* tomb,
+                   const uint32_t* val, const uint32_t* ids, uint64_t n, uint8_t* out_keys, uint64_t out_keys_cap,
+                   uint64_t* out_offsets, int64_t* out_created, uint8_t* out_tomb, uint32_t* out_val,
+                   uint64_t* key_bytes, hipStream_t s) {
+    if (!out_offsets) return fail(VBF_EINVAL, "out_offsets is NULL");
+    if (n && (!offsets || !ids)) return fail(VBF_EINVAL, "NULL argument");
+    if ((out_created && !created) || (out_tomb && !tomb) || (out_val && !val))
+        return fail(VBF_EINVAL, "an output array without its input");
+    size_t tmpb = 0;
+    HIP_TRY(vbf::scan_u64(nullptr, &tmpb, nullptr, nullptr, n + 1, s));
+    const uint64_t o_tmp = align256((n + 1) * 8);
+    void* ws = nullptr;
+    int rc = get_workspace(s, o_tmp + tmpb, &ws, kWsGather);
+    if (rc) return rc;
+    uint64_t* lens = static_cast<uint64_t*>(ws);
+    HIP_TRY(vbf::gather_lens(offsets, ids, n, lens, s));
+    HIP_TRY(vbf::scan_u64(static_cast<char*>(ws) + o_tmp, &tmpb, lens, out_offsets, n + 1, s));
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, out_offsets + n, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (key_bytes) *key_bytes = total;
+    if (total > out_keys_cap || (total && !out_keys))
+        return fail(VBF_EINVAL, "out_keys holds %llu < %llu bytes", (unsigned long long)out_keys_cap,
+                    (unsigned long long)total);
+    vbf::GatherArgs g{keys, offsets, created, tomb, val, ids, n, out_keys, out_offsets, out_created, out_tomb, out_val};
+    HIP_TRY(vbf::gather(g, s));
+    return VBF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int vbf_compact_merge_dev(const uint8_t* keys, const uint64_t* offsets, const int64_t* created_ms,
+                          const uint8_t* tombstones, const uint64_t* run_off, uint32_t nruns, const uint8_t* map_keys,
+                          const uint64_t* map_off, const int64_t* map_time, uint64_t map_n, int use_ttl,
+                          uint64_t entry_ttl_ms, uint64_t tombstone_ttl_ms, uint64_t now_ms, uint32_t* out_ids,
+                          uint64_t* n_out, uint32_t* upd_ids, int64_t* upd_time, uint64_t* n_upd, void* stream) {
+    int rc = compact_merge(keys, offsets, created_ms, tombstones, run_off, nruns, map_keys, map_off, map_time, map_n,
+                           use_ttl, entry_ttl_ms, tombstone_ttl_ms, now_ms, out_ids, n_out, upd_ids, upd_time, n_upd,
+                           (hipStream_t)stream);
+    return rc ? rc : ok();
+}
+
+int vbf_gather_entries_dev(const uint8_t* keys, const uint64_t* offsets, const int64_t* created_ms,
+                           const uint8_t* tombstones, const uint32_t* val_offsets, const uint32_t* ids, uint64_t n,
+                           uint8_t* out_keys, uint64_t out_keys_cap, uint64_t* out_offsets, int64_t* out_created_ms,
+                           uint8_t* out_tombstones, uint32_t* out_val_offsets, uint64_t* key_bytes, void* stream) {
+    int rc = gather_entries(keys, offsets, created_ms, tombstones, val_offsets, ids, n, out_keys, out_keys_cap,
+                            out_offsets, out_created_ms, out_tombstones, out_val_offsets, key_bytes, (hipStream_t)stream);
+    return rc ? rc : ok();
+}
+
+int vbf_compact_merge_host(const uint8_t* keys, const uint64_t* offsets, const int64_t* created_ms,
+                           const uint8_t* tombstones, const uint64_t* run_off, uint32_t nruns, const uint8_t* map_keys,
+                           const uint64_t* map_off, const int64_t* map_time, uint64_t map_n, int use_ttl,
+                           uint64_t entry_ttl_ms, uint64_t tombstone_ttl_ms, uint64_t now_ms, uint32_t* out_ids,
+                           uint64_t* n_out, uint32_t* upd_ids, int64_t* upd_time, uint64_t* n_upd, int device) {
+    if (!n_out) return fail(VBF_EINVAL, "n_out is NULL");
+    *n_out = 0;
+    if (n_upd) *n_upd = 0;
+    if (!nruns) return ok();
+    if (!run_off) return fail(VBF_EINVAL, "run_off is NULL");
+    const uint64_t total = run_off[nruns];
+    if (total && (!offsets || !created_ms || !tombstones || !out_ids)) return fail(VBF_EINVAL, "NULL argument");
+    if (map_n && (!map_keys || !map_off || !map_time)) return fail(VBF_EINVAL, "map arrays are NULL");
+    DEVICE_SCOPE(device);
+    hipStream_t s;
+    int rc = filter_stream(device, &s);
+    if (rc) return rc;
+    const uint64_t kb = total ? offsets[total] : 0, mkb = map_n ? map_off[map_n] : 0;
+    const uint64_t o_off = align256(kb), o_cr = o_off + align256((total + 1) * 8), o_tb = o_cr + align256(total * 8);
+    const uint64_t o_mk = o_tb + align256(total), o_mo = o_mk + align256(mkb), o_mt = o_mo + align256((map_n + 1) * 8);
+    const uint64_t o_ids = o_mt + align256(map_n * 8), o_ui = o_ids + align256(total * 4);
+    const uint64_t o_ut = o_ui + align256(total * 4), bytes = o_ut + align256(total * 8);
+    void* ws = nullptr;
+    if ((rc = get_workspace(s, bytes, &ws, kWsCompactIn))) return rc;
+    char* b = static_cast<char*>(ws);
+    if (kb) HIP_TRY(hipMemcpyAsync(b, keys, kb, hipMemcpyHostToDevice, s));
+    if (total) {
+        HIP_TRY(hipMemcpyAsync(b + o_off, offsets, (total + 1) * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(b + o_cr, created_ms, total * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(b + o_tb, tombstones, total, hipMemcpyHostToDevice, s));
+    }
+    if (map_n) {
+        if (mkb) HIP_TRY(hipMemcpyAsync(b + o_mk, map_keys, mkb, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(b + o_mo, map_off, (map_n + 1) * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(b + o_mt, map_time, map_n * 8, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    const bool want_upd = upd_ids && upd_time;
+    uint64_t nu = 0;
+    rc = compact_merge(reinterpret_cast<const uint8_t*>(b), reinterpret_cast<const uint64_t*>(b + o_off),
+                       reinterpret_cast<const int64_t*>(b + o_cr), reinterpret_cast<const uint8_t*>(b + o_tb), run_off,
+                       nruns, map_n ? reinterpret_cast<const uint8_t*>(b + o_mk) : nullptr,
+                       map_n ? reinterpret_cast<const uint64_t*>(b + o_mo) : nullptr,
+                       map_n ? reinterpret_cast<const int64_t*>(b + o_mt) : nullptr, map_n, use_ttl, entry_ttl_ms,
+                       tombstone_ttl_ms, now_ms, reinterpret_cast<uint32_t*>(b + o_ids), n_out,
+                       want_upd ? reinterpret_cast<uint32_t*>(b + o_ui) : nullptr,
+                       want_upd ? reinterpret_cast<int64_t*>(b + o_ut) : nullptr, &nu, s);
+    if (rc) return rc;
+    if (*n_out) HIP_TRY(hipMemcpyAsync(out_ids, b + o_ids, *n_out * 4, hipMemcpyDeviceToHost, s));
+    if (want_upd && nu) {
+        HIP_TRY(hipMemcpyAsync(upd_ids, b + o_ui, nu * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(upd_time, b + o_ut, nu * 8, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    if (n_upd) *n_upd = nu;
     return ok();
 }
 

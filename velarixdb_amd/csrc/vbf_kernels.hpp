@@ -82,6 +82,49 @@ struct MultiArgs {
     uint8_t* out;           // n * nsst
 };
 hipError_t launch_multi_probe(const MultiArgs& a, bool len_prefix, hipStream_t s);
+// Compaction merge (vbf_compact.hip).
+struct CompactArgs {
+    const uint8_t* keys;
+    const uint64_t* offsets;  // arena: entry e = keys[offsets[e] .. offsets[e+1])
+    const int64_t* created;   // ms
+    const uint8_t* tomb;
+    const uint64_t* run_off;  // device, nruns + 1 entry boundaries (run_off[0] = 0)
+    uint32_t nruns;
+    const uint8_t* map_keys;  // tombstone map: sorted unique keys
+    const uint64_t* map_off;
+    const int64_t* map_time;
+    uint64_t map_n;
+    int use_ttl;
+    uint64_t entry_ttl_ms, tomb_ttl_ms, now_ms;
+    uint64_t run_off_host_total;  // entries in all runs (host side)
+};
+struct GatherArgs {
+    const uint8_t* keys;
+    const uint64_t* offsets;
+    const int64_t* created;
+    const uint8_t* tomb;
+    const uint32_t* val;
+    const uint32_t* ids;
+    uint64_t n;
+    uint8_t* out_keys;
+    const uint64_t* out_off;
+    int64_t* out_created;
+    uint8_t* out_tomb;
+    uint32_t* out_val;
+};
+hipError_t launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t s);
+hipError_t compact_check_sorted(const CompactArgs& a, uint32_t* err, hipStream_t s);
+hipError_t compact_merge_levels(const CompactArgs& a, const uint64_t* d_bnd_all, const uint32_t* nseg_per_level,
+                                uint32_t nlevels, uint32_t* ping, uint32_t* pong, uint32_t** result, hipStream_t s);
+hipError_t compact_fold(const CompactArgs& a, const uint32_t* order, uint64_t total, uint8_t* keep, uint32_t* sel,
+                        uint8_t* upd, int64_t* upd_time, hipStream_t s);
+hipError_t select_u32(void* tmp, size_t* bytes, const uint32_t* in, const uint8_t* flags, uint32_t* out,
+                      uint64_t* nsel, uint64_t n, hipStream_t s);
+hipError_t select_i64(void* tmp, size_t* bytes, const int64_t* in, const uint8_t* flags, int64_t* out,
+                      uint64_t* nsel, uint64_t n, hipStream_t s);
+hipError_t gather_lens(const uint64_t* offsets, const uint32_t* ids, uint64_t n, uint64_t* lens, hipStream_t s);
+hipError_t scan_u64(void* tmp, size_t* bytes, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s);
+hipError_t gather(const GatherArgs& g, hipStream_t s);
 hipError_t gen_sst_fixed(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* data, uint32_t* blocks,
                          hipStream_t s);
 }  // namespace vbf
