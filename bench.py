@@ -380,7 +380,8 @@ def bench_sst(ctx, args):
                       % (n // 10**6, data.numel() / 1e9, nb, bf.num_bits(), bf.no_of_hash_func)},
            "decode_only": {"ms_per_step": dwall / args.steps * 1e3,
                            "entries_per_s": n * args.steps / dwall,
-                           "data_gb_per_s": data.numel() * args.steps / dwall / 1e9},
+                           "data_gb_per_s": data.numel() * args.steps / dwall / 1e9,
+                           "phases": phase_report(dph, args.steps)},
            "phases": phase_report(rph, args.steps)}
     if ctx.world == 1 and ctx.rank == 0 and not args.no_cpu_baseline:
         import oracle

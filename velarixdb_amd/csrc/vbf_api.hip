@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdarg>
+#include <cstdlib>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -384,19 +385,25 @@ namespace {
 inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 
 int sst_count_pass(const uint8_t* data, uint64_t len, const uint32_t* blocks, uint64_t nblocks,
-                   hipStream_t s, vbf::SstArgs* a, uint64_t* n_out) {
+                   hipStream_t s, vbf::SstArgs* a, uint64_t* n_out, uint32_t* uniform_len = nullptr) {
     *a = vbf::SstArgs{};
     *n_out = 0;
+    if (uniform_len) *uniform_len = 0xFFFFFFFFu;
     if (len && (!data || !blocks || !nblocks))
         return fail(VBF_EINVAL, "data.db of %llu bytes needs its block start offsets (index.db)",
                     (unsigned long long)len);
     if (!len && nblocks) return fail(VBF_EINVAL, "%llu block offsets for an empty data.db", (unsigned long long)nblocks);
     if (nblocks >= 0x7FFFFFFFull) return fail(VBF_EINVAL, "too many blocks (%llu)", (unsigned long long)nblocks);
     if (!len) return VBF_OK;
-    size_t tmpb = 0;
+    size_t tmpb = 0, tmpr = 0;
     HIP_TRY(vbf::sst_scan(nullptr, nullptr, nblocks + 1, nullptr, &tmpb, s));
+    HIP_TRY(vbf::sst_len_range(nullptr, nullptr, nblocks, nullptr, nullptr, &tmpr, s));
+    tmpb = std::max(tmpb, tmpr);
     const uint64_t o_ebase = align256((nblocks + 1) * 4);
-    const uint64_t o_err = o_ebase + align256((nblocks + 1) * 8);
+    const uint64_t o_pos = o_ebase + align256((nblocks + 1) * 8);
+    const uint64_t o_lmin = o_pos + align256(vbf::sst_pos_bytes(nblocks));
+    const uint64_t o_lmax = o_lmin + align256(nblocks * 4);
+    const uint64_t o_err = o_lmax + align256(nblocks * 4);
     const uint64_t o_tmp = o_err + 256;
     void* ws = nullptr;
     int rc = get_workspace(s, o_tmp + tmpb, &ws, kWsSstScratch);
@@ -407,24 +414,35 @@ int sst_count_pass(const uint8_t* data, uint64_t len, const uint32_t* blocks, ui
     uint32_t* err = reinterpret_cast<uint32_t*>(base + o_err);
     HIP_TRY(hipMemsetAsync(counts, 0, (nblocks + 1) * 4, s));
     HIP_TRY(hipMemsetAsync(err, 0, 4, s));
-    HIP_TRY(hipMemsetAsync(err + 1, 0xFF, 4, s));
-    *a = vbf::SstArgs{data, len, blocks, nblocks, counts, ebase, nullptr, nullptr, nullptr, nullptr, nullptr, err};
+    HIP_TRY(hipMemsetAsync(err + 1, 0xFF, 12, s));
+    uint16_t* pos = reinterpret_cast<uint16_t*>(base + o_pos);
+    static const uint32_t abl = [] { const char* e = getenv("VBF_ABLATE"); return e ? (uint32_t)atoi(e) : 0u; }();
+    uint32_t* lmin = reinterpret_cast<uint32_t*>(base + o_lmin);
+    uint32_t* lmax = reinterpret_cast<uint32_t*>(base + o_lmax);
+    *a = vbf::SstArgs{data, len, blocks, nblocks, counts, pos, lmin, lmax, ebase, nullptr, nullptr, nullptr, nullptr,
+                      nullptr, err, abl};
+    vbf::phase_begin(vbf::kPhaseSstWalk, s);
     HIP_TRY(vbf::sst_count(*a, s));
+    vbf::phase_end(vbf::kPhaseSstWalk, s);
+    vbf::phase_begin(vbf::kPhaseSstScan, s);
     HIP_TRY(vbf::sst_scan(counts, ebase, nblocks + 1, base + o_tmp, &tmpb, s));
+    if (uniform_len) HIP_TRY(vbf::sst_len_range(lmin, lmax, nblocks, err + 2, base + o_tmp, &tmpb, s));
+    vbf::phase_end(vbf::kPhaseSstScan, s);
     uint64_t total = 0;
-    uint32_t ev[2] = {0, 0};
+    uint32_t ev[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(&total, ebase + nblocks, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(ev, err, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(ev, err, 16, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (ev[0]) {
         const char* what = (ev[0] & 8) ? "block offsets not increasing / not starting at 0 / past the end"
-                         : (ev[0] & 4) ? "block larger than 8192 bytes"
-                         : (ev[0] & 2) ? "more than 512 entries in a block"
+                         : (ev[0] & 4) ? "block larger than 65535 bytes"
+                         : (ev[0] & 2) ? "more than 256 entries in a block"
                                        : "entry crosses the block end (truncated data.db or wrong index)";
         return fail(VBF_EINVAL, "malformed data.db at block %u: %s", ev[1], what);
     }
     if (len < 17 * total) return fail(VBF_EINVAL, "inconsistent entry count %llu", (unsigned long long)total);
     *n_out = total;
+    if (uniform_len && total && ev[2] == ev[3] && a->ablate == 0) *uniform_len = ev[2];
     return VBF_OK;
 }
 
@@ -441,7 +459,9 @@ int sst_emit_pass(vbf::SstArgs a, uint8_t* keys, uint64_t* offsets, uint32_t* va
     a.created = created;
     a.tomb = tomb;
     if (!keys && !offsets && !val_off && !created && !tomb) return VBF_OK;
+    vbf::phase_begin(vbf::kPhaseSstEmit, s);
     HIP_TRY(vbf::sst_emit(a, s));
+    vbf::phase_end(vbf::kPhaseSstEmit, s);
     return VBF_OK;
 }
 
@@ -1015,7 +1035,8 @@ int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t
     hipStream_t st = (hipStream_t)stream;
     uint64_t n = 0;
     vbf::SstArgs a;
-    int rc = sst_count_pass(data, len, blocks, nblocks, st, &a, &n);
+    uint32_t ulen = 0xFFFFFFFFu;
+    int rc = sst_count_pass(data, len, blocks, nblocks, st, &a, &n, &ulen);
     if (rc) return rc;
     if (n_out) *n_out = n;
     if ((rc = check_mk(s.m, f->k, n))) return rc;
@@ -1025,9 +1046,12 @@ int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t
         if ((rc = get_workspace(st, o_off + (n + 1) * 8, &out, kWsSstKeys))) return rc;
         uint8_t* d_keys = static_cast<uint8_t*>(out);
         uint64_t* d_off = reinterpret_cast<uint64_t*>(d_keys + o_off);
-        if ((rc = sst_emit_pass(a, d_keys, d_off, nullptr, nullptr, nullptr, st))) return rc;
+        // every key the same length (the common case): packed keys are a fixed-stride batch, which
+        // the build reads with its aligned fast path instead of through offsets
+        const bool uniform = ulen != 0xFFFFFFFFu && ulen > 0;
+        if ((rc = sst_emit_pass(a, d_keys, uniform ? nullptr : d_off, nullptr, nullptr, nullptr, st))) return rc;
         std::lock_guard<std::mutex> lk(s.mu);
-        vbf::KeyBatch kb2 = batch(d_keys, d_off, 0, 0, n, 1);
+        vbf::KeyBatch kb2 = uniform ? batch(d_keys, nullptr, 0, ulen, n, 1) : batch(d_keys, d_off, 0, 0, n, 1);
         if ((rc = do_build(kb2, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, st))) return rc;
     }
     f->n.fetch_add((uint32_t)n);

@@ -21,7 +21,7 @@ hipError_t launch_build(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* wo
 
 // Optional per-phase timing (vbf_profile_*): HIP events recorded on the launch stream.
 enum Phase { kPhaseTileSort = 0, kPhaseTranspose = 1, kPhaseSegOr = 2, kPhaseAtomicBuild = 3,
-             kPhaseProbe = 4, kNumPhases = 5 };
+             kPhaseProbe = 4, kPhaseSstWalk = 5, kPhaseSstScan = 6, kPhaseSstEmit = 7, kNumPhases = 8 };
 void phase_begin(int phase, hipStream_t s);
 void phase_end(int phase, hipStream_t s);
 
@@ -52,17 +52,24 @@ struct SstArgs {
     uint64_t len;
     const uint32_t* blocks;  // block start offsets (index.db)
     uint64_t nblocks;
-    uint32_t* counts;        // [nblocks + 1] entry counts (count pass)
+    uint32_t* counts;        // [nblocks + 1] entry counts (walk pass)
+    uint16_t* pos;           // [nblocks * 256] entry starts within each block (walk pass)
+    uint32_t* lmin;          // [nblocks] shortest / longest key per block (walk pass)
+    uint32_t* lmax;
     const uint64_t* ebase;   // [nblocks + 1] exclusive scan of counts (emit pass)
     uint8_t* keys;
     uint64_t* offsets;       // [n + 1] absolute positions in keys
     uint32_t* val_off;
     uint64_t* created;
     uint8_t* tomb;
-    uint32_t* err;           // [0] error bits, [1] first bad block
+    uint32_t* err;           // [0] error bits, [1] first bad block, [2]/[3] min/max key length
+    uint32_t ablate;         // timing experiments only (VBF_ABLATE 11/12)
 };
 hipError_t sst_count(const SstArgs& a, hipStream_t s);
 hipError_t sst_emit(const SstArgs& a, hipStream_t s);
+uint64_t sst_pos_bytes(uint64_t nblocks);
+hipError_t sst_len_range(const uint32_t* lmin, const uint32_t* lmax, uint64_t nblocks, uint32_t* out2, void* tmp,
+                         size_t* tmp_bytes, hipStream_t s);
 hipError_t sst_scan(const uint32_t* counts, uint64_t* ebase, uint64_t nblocks, void* tmp, size_t* tmp_bytes,
                     hipStream_t s);
 // Batched probe across SSTs (vbf_multi.hip).

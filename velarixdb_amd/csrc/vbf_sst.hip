@@ -11,191 +11,293 @@
 // block's start offset (table.rs:331-338, index/indexer.rs:151-170).  That index is what makes
 // the decode parallel: one wavefront per block.
 //
-//   k_sst_blocks<EMIT=false>: stage the block in LDS (coalesced dword loads), walk its entry
-//                             chain (a dependent chain of u32 reads, but out of LDS), write the
-//                             entry count.  A malformed block (an entry crossing the block end,
-//                             more than kMaxEnt entries, a block over kStage bytes) sets the
-//                             error word instead.
+//   k_sst_walk : stage the block in LDS (all of a lane's 16-byte loads in flight at once), walk
+//                its entry chain (a dependent chain of u32 reads out of LDS, wave-uniform, scalar
+//                control), write the entry starts (u16, 256 slots per block) and the count.  A
+//                malformed block (an entry crossing the block end, more than 256 entries, a
+//                block over 64 KiB, offsets out of order) sets the error word instead.
 //   exclusive scan of the counts (hipcub) -> entry base E_b of every block; the block's key
-//                             bytes start at G_b = start_b - 17 * E_b (all bytes before it are
-//                             entries).
-//   k_sst_blocks<EMIT=true> : stage + walk again, then lanes write the entry arrays (one lane per
-//                             entry) and the packed key bytes (one lane per aligned output dword,
-//                             source found by a binary search over the entry starts in LDS).
+//                bytes start at G_b = start_b - 17 * E_b (all bytes before it are entries).
+//   k_sst_emit : stage the block again, no walk: lanes write the entry arrays (one lane per
+//                entry) and the packed key bytes (one lane per aligned output dword, source
+//                entry found by a binary search over the entry starts in LDS).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <hipcub/device/device_reduce.hpp>
 #include <hipcub/device/device_scan.hpp>
 
 #include "vbf_kernels.hpp"
 
 namespace vbf {
 
-constexpr int kSstWaves = 4;            // waves per workgroup; one block per wave
-constexpr uint32_t kStage = 8192;       // bytes of a block a wave stages (writer max: 4096)
-constexpr uint32_t kMaxEnt = 512;       // entries per block (writer max: 4096 / 17 = 240)
-constexpr uint32_t kEntryFixed = 17;    // key_len + value offset + created_at + tombstone
+constexpr int kSstWaves = 4;             // waves per workgroup; one block per wave
+constexpr uint32_t kStage = 4096 + 64;   // bytes a wave stages in LDS (writer max block: 4096)
+constexpr uint32_t kChunks = (kStage + 16 + 1023) / 1024;  // 16-byte loads per lane to stage
+constexpr uint32_t kMaxEnt = 256;        // entries per block (writer max: 4096 / 17 = 240)
+constexpr uint32_t kMaxBlock = 65535;    // larger blocks (never written by the reference) fail
+constexpr uint32_t kEntryFixed = 17;     // key_len + value offset + created_at + tombstone
 
 enum : uint32_t { kSstErrCross = 1, kSstErrDense = 2, kSstErrBig = 4, kSstErrOrder = 8 };
 
-// u32 at byte offset `o` of an LDS byte image held as dwords (unaligned: two reads + alignbyte).
-__device__ __forceinline__ uint32_t lds_u32(const uint32_t* buf, uint32_t o) {
-    const uint32_t w0 = buf[o >> 2], w1 = buf[(o >> 2) + 1];
-    return __builtin_amdgcn_alignbyte(w1, w0, o & 3);
-}
-__device__ __forceinline__ uint32_t lds_u8(const uint32_t* buf, uint32_t o) {
-    return (buf[o >> 2] >> ((o & 3) * 8)) & 0xFFu;
+// A block's bytes: staged in LDS (16-byte aligned image, block byte x at img byte sh + x) or,
+// for a block larger than kStage, read in place from global memory.
+struct BlockView {
+    const uint32_t* lds;
+    const uint8_t* glb;
+    uint32_t sh;
+    __device__ __forceinline__ uint32_t u32(uint32_t x) const {
+        if (lds) {
+            const uint32_t o = sh + x, w0 = lds[o >> 2], w1 = lds[(o >> 2) + 1];
+            return __builtin_amdgcn_alignbyte(w1, w0, o & 3);
+        }
+        return (uint32_t)glb[x] | ((uint32_t)glb[x + 1] << 8) | ((uint32_t)glb[x + 2] << 16) |
+               ((uint32_t)glb[x + 3] << 24);
+    }
+    __device__ __forceinline__ uint32_t u8(uint32_t x) const {
+        if (lds) {
+            const uint32_t o = sh + x;
+            return (lds[o >> 2] >> ((o & 3) * 8)) & 0xFFu;
+        }
+        return glb[x];
+    }
+};
+
+__device__ __forceinline__ void sst_error(const SstArgs& a, uint64_t b, uint32_t bits) {
+    atomicOr(a.err, bits);
+    atomicMin(a.err + 1, (uint32_t)std::min<uint64_t>(b, 0xFFFFFFFFu));
 }
 
-template <bool EMIT>
-__global__ __launch_bounds__(64 * kSstWaves) void k_sst_blocks(SstArgs a) {
-    __shared__ uint32_t stage[kSstWaves][kStage / 4 + 2];
-    __shared__ uint16_t pos[kSstWaves][kMaxEnt];
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t b = (uint64_t)blockIdx.x * kSstWaves + wave;
-    uint32_t* buf = stage[wave];
-    uint16_t* ps = pos[wave];
-    if (b >= a.nblocks) return;  // no workgroup barriers below: each wave is independent
-
-    const uint64_t s = a.blocks[b];
+// Block b's byte range; false (error recorded) when the offsets are out of order.
+__device__ __forceinline__ bool block_range(const SstArgs& a, uint64_t b, uint64_t& s, uint32_t& blen, uint32_t lane) {
+    s = a.blocks[b];
     const uint64_t e = b + 1 < a.nblocks ? a.blocks[b + 1] : a.len;
     if (e <= s || e > a.len || (b == 0 && s != 0)) {
-        if (lane == 0) {
-            atomicOr(a.err, kSstErrOrder);
-            atomicMin(a.err + 1, (uint32_t)std::min<uint64_t>(b, 0xFFFFFFFFu));
-        }
-        return;
+        if (lane == 0) sst_error(a, b, kSstErrOrder);
+        return false;
     }
-    const uint32_t blen = (uint32_t)std::min<uint64_t>(e - s, kStage + 1);
-    if (blen > kStage) {
-        if (lane == 0) {
-            atomicOr(a.err, kSstErrBig);
-            atomicMin(a.err + 1, (uint32_t)std::min<uint64_t>(b, 0xFFFFFFFFu));
-        }
-        return;
+    if (e - s > kMaxBlock) {
+        if (lane == 0) sst_error(a, b, kSstErrBig);
+        return false;
     }
-    // stage [s & ~3, e) as dwords; byte x of the block is at buf byte sh + x
-    const uint64_t a0 = s & ~3ull;
+    blen = (uint32_t)(e - s);
+    return true;
+}
+
+// Stage [s & ~15, s + blen) into LDS with every 16-byte load of the lane in flight at once.
+__device__ __forceinline__ BlockView stage_block(const SstArgs& a, uint64_t s, uint32_t blen, uint32_t* buf,
+                                                 uint32_t lane) {
+    if (blen > kStage) return BlockView{nullptr, a.data + s, 0};
+    const uint64_t a0 = s & ~15ull;
     const uint32_t sh = (uint32_t)(s - a0);
-    const uint32_t nw = (sh + blen + 3) / 4;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.data + a0);
-    for (uint32_t w = lane; w < nw; w += 64) {
-        const uint64_t g = a0 + 4ull * w;
-        uint32_t v;
-        if (g + 4 <= a.len) {
-            v = src[w];
-        } else {
-            v = 0;
-            for (uint32_t t = 0; t < 4; ++t)
-                if (g + t < a.len) v |= (uint32_t)a.data[g + t] << (8 * t);
-        }
-        buf[w] = v;
+    const uint32_t nc = (sh + blen + 15) / 16;
+    uint4 v[kChunks];
+#pragma unroll
+    for (uint32_t c = 0; c < kChunks; ++c) {  // all full chunks in flight together
+        const uint32_t q = lane + 64 * c;
+        const uint64_t g = a0 + 16ull * q;
+        v[c] = make_uint4(0, 0, 0, 0);
+        if (q < nc && g + 16 <= a.len) v[c] = *reinterpret_cast<const uint4*>(a.data + g);
     }
-    if (lane == 0) buf[nw] = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < kChunks; ++c) {
+        const uint32_t q = lane + 64 * c;
+        const uint64_t g = a0 + 16ull * q;
+        if (q < nc && g + 16 > a.len) {  // the file's last, partial chunk
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (uint32_t t = 0; t < 16; ++t)
+                if (g + t < a.len) w[t >> 2] |= (uint32_t)a.data[g + t] << (8 * (t & 3));
+            v[c] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < kChunks; ++c) {
+        const uint32_t q = lane + 64 * c;
+        if (q < nc) *reinterpret_cast<uint4*>(buf + 4 * q) = v[c];
+    }
+    if (lane == 0) buf[4 * nc] = 0;  // u32() of the last bytes reads one dword past them
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return BlockView{buf, nullptr, sh};
+}
 
-    // walk the entry chain (every lane in step: same LDS addresses, broadcast reads)
-    uint32_t p = 0, n = 0, bad = 0;
-    while (p < blen) {
-        if (blen - p < 4) {
-            bad = kSstErrCross;
-            break;
+// Pass 1: walk each block's entry chain, record the entry starts (u16, kMaxEnt slots per block)
+// and the count.  The chain is wave-uniform: its state lives in scalar registers (readfirstlane),
+// so a step is one ds_read2 + a handful of SALU ops; entry starts collect in four VGPR slots
+// (entry i -> lane i % 64, slot i / 64) and leave with coalesced stores.
+template <bool LDS>
+__device__ __forceinline__ uint32_t walk_chain(const BlockView& v, uint32_t blen, uint32_t lane, uint32_t (&pr)[4],
+                                               uint32_t& bad, uint32_t& lmin, uint32_t& lmax) {
+    // Lean loop: no per-step checks.  An entry whose length runs past the block end pushes p
+    // beyond blen (a key over 64 KiB cannot fit a block: p jumps to 2^17); the walk is valid iff
+    // it ends exactly at blen.  Entry starts go to lane i of slot k by v_writelane.
+    uint32_t p = 0, n = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        for (uint32_t i = 0; i < 64 && p < blen; ++i) {
+            uint32_t L;
+            if constexpr (LDS) {
+                const uint32_t o = v.sh + p, w0 = v.lds[o >> 2], w1 = v.lds[(o >> 2) + 1];
+                L = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbyte(w1, w0, o & 3));
+            } else {
+                L = blen - p >= 4 ? __builtin_amdgcn_readfirstlane(v.u32(p)) : 0x10000u;
+            }
+            asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(pr[k]) : "s"(p), "s"(i) : "m0");
+            p = L > 0xFFFFu ? 0x20000u : p + L + kEntryFixed;
+            lmin = std::min(lmin, L);
+            lmax = std::max(lmax, L);
+            ++n;
         }
-        const uint32_t L = lds_u32(buf, sh + p);
-        if ((uint64_t)blen - p - 4 < (uint64_t)L + 13) {
-            bad = kSstErrCross;
-            break;
+    }
+    bad = p != blen ? (p < blen ? kSstErrDense : kSstErrCross) : 0;
+    (void)lane;
+    return n;
+}
+
+__global__ __launch_bounds__(64 * kSstWaves) void k_sst_walk(SstArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kSstWaves][kStage / 4 + 8];
+    const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t b = (uint64_t)blockIdx.x * kSstWaves + wave;
+    if (b >= a.nblocks) return;  // no workgroup barriers: waves are independent
+    uint64_t s;
+    uint32_t blen;
+    if (!block_range(a, b, s, blen, lane)) return;
+    BlockView v;
+    if (a.ablate == 12 || a.ablate == 13) v = BlockView{stage[wave], nullptr, 0};  // timing: no staging
+    else v = stage_block(a, s, blen, stage[wave], lane);
+    uint32_t pr[4] = {0, 0, 0, 0}, bad = 0, lmin = 0xFFFFFFFFu, lmax = 0;
+    uint32_t n = 0;
+    if (a.ablate == 11) {  // timing experiment: staging only, no walk
+        n = (stage[wave][lane] == 0x12345678u) ? 1 : 0;
+    } else if (a.ablate == 13 || a.ablate == 14) {  // dependent LDS chain of 124 steps
+        uint32_t o = 0;
+        for (uint32_t i = 0; i < 124; ++i) {
+            const uint32_t w = stage[wave][(o >> 2) & 1023];
+            o = __builtin_amdgcn_readfirstlane(o + 33 + (w & 0x80000000u ? 1 : 0));
         }
-        if (n == kMaxEnt) {
-            bad = kSstErrDense;
-            break;
+        pr[0] = o;
+        n = 124;
+    } else if (a.ablate == 12) {  // walk a synthetic chain of 124 entries
+        for (uint32_t i = 0; i < 124; ++i) {
+            const uint32_t o = i * 33 + (stage[wave][i & 15] & 1);
+            pr[i & 3] += __builtin_amdgcn_readfirstlane(o);
         }
-        if (EMIT && lane == 0) ps[n] = (uint16_t)p;
-        p += L + kEntryFixed;
-        ++n;
+        n = 124;
+    } else {
+        n = v.lds ? walk_chain<true>(v, blen, lane, pr, bad, lmin, lmax)
+                  : walk_chain<false>(v, blen, lane, pr, bad, lmin, lmax);
     }
     if (bad) {
-        if (lane == 0) {
-            atomicOr(a.err, bad);
-            atomicMin(a.err + 1, (uint32_t)std::min<uint64_t>(b, 0xFFFFFFFFu));
-        }
+        if (lane == 0) sst_error(a, b, bad);
         return;
     }
-    if constexpr (!EMIT) {
-        if (lane == 0) a.counts[b] = n;
-        return;
-    } else {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint64_t E = a.ebase[b];
-        const uint64_t G = s - (uint64_t)kEntryFixed * E;  // key bytes before this block
-        // per-entry arrays
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t q = ps[i];
-            const uint32_t L = lds_u32(buf, sh + q);
-            if (a.offsets) a.offsets[E + i] = G + q - kEntryFixed * i;
-            if (a.val_off) a.val_off[E + i] = lds_u32(buf, sh + q + 4 + L);
-            if (a.created) {
-                const uint64_t lo = lds_u32(buf, sh + q + 8 + L), hi = lds_u32(buf, sh + q + 12 + L);
-                a.created[E + i] = lo | (hi << 32);
-            }
-            if (a.tomb) a.tomb[E + i] = lds_u8(buf, sh + q + 16 + L) == 1;
+    uint16_t* out = a.pos + b * kMaxEnt;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        if (lane + 64 * k < n) out[lane + 64 * k] = (uint16_t)pr[k];
+    if (lane == 0) {
+        a.counts[b] = n;
+        a.lmin[b] = lmin;  // key-length range (reduced after the pass): uniform lengths let the
+        a.lmax[b] = lmax;  // build use the fixed-stride key path
+    }
+}
+
+// Pass 2: no walk -- stage the block again, read its entry starts, write the outputs.
+__global__ __launch_bounds__(64 * kSstWaves) void k_sst_emit(SstArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kSstWaves][kStage / 4 + 8];
+    __shared__ uint16_t pos[kSstWaves][kMaxEnt];
+    const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t b = (uint64_t)blockIdx.x * kSstWaves + wave;
+    if (b >= a.nblocks) return;
+    const uint64_t s = a.blocks[b];
+    const uint32_t blen = (uint32_t)((b + 1 < a.nblocks ? a.blocks[b + 1] : a.len) - s);  // validated by pass 1
+    const uint32_t n = a.counts[b];
+    uint16_t* ps = pos[wave];
+    const uint16_t* pin = a.pos + b * kMaxEnt;
+    for (uint32_t i = lane; i < n; i += 64) ps[i] = pin[i];
+    const BlockView v = stage_block(a, s, blen, stage[wave], lane);  // its barrier covers ps too
+    const uint64_t E = a.ebase[b];
+    const uint64_t G = s - (uint64_t)kEntryFixed * E;  // key bytes before this block
+    for (uint32_t i = lane; i < n; i += 64) {
+        const uint32_t q = ps[i];
+        const uint32_t L = v.u32(q);
+        if (a.offsets) a.offsets[E + i] = G + q - kEntryFixed * i;
+        if (a.val_off) a.val_off[E + i] = v.u32(q + 4 + L);
+        if (a.created) a.created[E + i] = (uint64_t)v.u32(q + 8 + L) | ((uint64_t)v.u32(q + 12 + L) << 32);
+        if (a.tomb) a.tomb[E + i] = v.u8(q + 16 + L) == 1;
+    }
+    const uint64_t K = blen - (uint64_t)kEntryFixed * n;  // this block's key bytes
+    if (a.offsets && b + 1 == a.nblocks && lane == 0) a.offsets[E + n] = G + K;
+    if (!a.keys || K == 0) return;
+    // packed key bytes [G, G + K), one lane per aligned output dword: output byte d lies in the
+    // last entry i with cum(i) = pos(i) - 17 i <= d, at block byte d + 4 + 17 i
+    auto cum = [&](uint32_t i) { return (uint32_t)ps[i] - kEntryFixed * i; };
+    const uint64_t w_lo = G >> 2, w_hi = (G + K + 3) >> 2;
+    uint32_t hint = 0;  // lanes move forward through the block: start the search at the last hit
+    for (uint64_t w = w_lo + lane; w < w_hi; w += 64) {
+        const uint64_t g0 = w << 2;
+        const uint32_t d0 = g0 < G ? 0 : (uint32_t)(g0 - G);
+        uint32_t lo = hint, hi = n - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (cum(mid) <= d0) lo = mid;
+            else hi = mid - 1;
         }
-        const uint64_t K = blen - (uint64_t)kEntryFixed * n;  // this block's key bytes
-        if (a.offsets && b + 1 == a.nblocks && lane == 0) a.offsets[E + n] = G + K;
-        if (!a.keys || K == 0) return;
-        // packed key bytes [G, G + K): lane per aligned output dword.  Output byte d of the
-        // block lies in entry i = the last entry with cum(i) = pos(i) - 17 i <= d, at block byte
-        // d + 4 + 17 i.
-        auto cum = [&](uint32_t i) { return (uint32_t)ps[i] - kEntryFixed * i; };
-        const uint64_t w_lo = G >> 2, w_hi = (G + K + 3) >> 2;
-        for (uint64_t w = w_lo + lane; w < w_hi; w += 64) {
-            const uint64_t g0 = w << 2;
-            const uint32_t d0 = g0 < G ? 0 : (uint32_t)(g0 - G);  // first byte of the dword in range
-            uint32_t lo = 0, hi = n - 1;                          // last i with cum(i) <= d0
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) >> 1;
-                if (cum(mid) <= d0) lo = mid;
-                else hi = mid - 1;
-            }
-            uint32_t i = lo;
-            const bool full = g0 >= G && g0 + 4 <= G + K;
-            const uint32_t next = i + 1 < n ? cum(i + 1) : (uint32_t)K;
-            if (full && d0 + 4 <= next) {  // whole dword inside one key
-                reinterpret_cast<uint32_t*>(a.keys)[w] = lds_u32(buf, sh + d0 + 4 + kEntryFixed * i);
-                continue;
-            }
-            uint32_t v = 0;
-            for (uint32_t t = 0; t < 4; ++t) {
-                const uint64_t g = g0 + t;
-                if (g < G || g >= G + K) continue;
-                const uint32_t d = (uint32_t)(g - G);
-                while (i + 1 < n && cum(i + 1) <= d) ++i;
-                const uint32_t byte = lds_u8(buf, sh + d + 4 + kEntryFixed * i);
-                if (full) v |= byte << (8 * t);
-                else a.keys[g] = (uint8_t)byte;
-            }
-            if (full) reinterpret_cast<uint32_t*>(a.keys)[w] = v;
+        uint32_t i = lo;
+        hint = lo;
+        const bool full = g0 >= G && g0 + 4 <= G + K;
+        const uint32_t next = i + 1 < n ? cum(i + 1) : (uint32_t)K;
+        if (full && d0 + 4 <= next) {
+            reinterpret_cast<uint32_t*>(a.keys)[w] = v.u32(d0 + 4 + kEntryFixed * i);
+            continue;
         }
+        uint32_t val = 0;
+        for (uint32_t t = 0; t < 4; ++t) {
+            const uint64_t g = g0 + t;
+            if (g < G || g >= G + K) continue;
+            const uint32_t d = (uint32_t)(g - G);
+            while (i + 1 < n && cum(i + 1) <= d) ++i;
+            const uint32_t byte = v.u8(d + 4 + kEntryFixed * i);
+            if (full) val |= byte << (8 * t);
+            else a.keys[g] = (uint8_t)byte;
+        }
+        if (full) reinterpret_cast<uint32_t*>(a.keys)[w] = val;
     }
 }
 
 hipError_t sst_count(const SstArgs& a, hipStream_t s) {
     if (a.nblocks == 0) return hipSuccess;
     const uint64_t grid = (a.nblocks + kSstWaves - 1) / kSstWaves;
-    hipLaunchKernelGGL(k_sst_blocks<false>, dim3((uint32_t)grid), dim3(64 * kSstWaves), 0, s, a);
+    hipLaunchKernelGGL(k_sst_walk, dim3((uint32_t)grid), dim3(64 * kSstWaves), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t sst_emit(const SstArgs& a, hipStream_t s) {
     if (a.nblocks == 0) return hipSuccess;
     const uint64_t grid = (a.nblocks + kSstWaves - 1) / kSstWaves;
-    hipLaunchKernelGGL(k_sst_blocks<true>, dim3((uint32_t)grid), dim3(64 * kSstWaves), 0, s, a);
+    hipLaunchKernelGGL(k_sst_emit, dim3((uint32_t)grid), dim3(64 * kSstWaves), 0, s, a);
     return hipGetLastError();
+}
+
+uint64_t sst_pos_bytes(uint64_t nblocks) { return nblocks * kMaxEnt * 2; }
+
+hipError_t sst_len_range(const uint32_t* lmin, const uint32_t* lmax, uint64_t nblocks, uint32_t* out2, void* tmp,
+                         size_t* tmp_bytes, hipStream_t s) {
+    size_t need = 0, b1 = 0;
+    hipError_t e = hipcub::DeviceReduce::Min(nullptr, need, lmin, out2, (int)nblocks, s);
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceReduce::Max(nullptr, b1, lmax, out2 + 1, (int)nblocks, s);
+    if (e != hipSuccess) return e;
+    need = std::max(need, b1);
+    if (!tmp) {
+        *tmp_bytes = need;
+        return hipSuccess;
+    }
+    e = hipcub::DeviceReduce::Min(tmp, need, lmin, out2, (int)nblocks, s);
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceReduce::Max(tmp, need, lmax, out2 + 1, (int)nblocks, s);
 }
 
 hipError_t sst_scan(const uint32_t* counts, uint64_t* ebase, uint64_t nblocks, void* tmp, size_t* tmp_bytes,
