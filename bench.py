@@ -398,6 +398,99 @@ def bench_sst(ctx, args):
     return res
 
 
+def bench_compact(ctx, args):
+    """one bucket of 4 sorted tables x 25M 16-byte keys (half of each table's
+    keys also in another table, 5 % tombstones) through the fold (vbf_compact_merge_dev), then the
+    gather into the build's layout and the merged table's filter build (sized.rs:170-200)."""
+    nr, per = 4, args.keys // 4
+    L = 16
+    j = torch.arange(per, device=ctx.dev, dtype=torch.int64)
+    ks, cr, tb = [], [], []
+    g = torch.Generator(device=ctx.dev)
+    g.manual_seed(7)
+    for r in range(nr):
+        v = 2 * j + (r % 2) + (per * (r // 2))  # tables 0/2 and 1/3 overlap by half
+        be = v.view(torch.uint8).view(-1, 8).flip(1)
+        ks.append(torch.cat([be, be], dim=1).reshape(-1))
+        cr.append(torch.randint(0, 1 << 40, (per,), device=ctx.dev, generator=g))
+        tb.append((torch.rand(per, device=ctx.dev, generator=g) < 0.05).to(torch.uint8))
+    keys, created, tomb = torch.cat(ks), torch.cat(cr), torch.cat(tb)
+    offs = torch.arange(nr * per + 1, device=ctx.dev, dtype=torch.int64) * L
+    run_off = (np.arange(nr + 1, dtype=np.uint64) * per)
+    ids = torch.empty(nr * per, dtype=torch.int32, device=ctx.dev)
+    mk = torch.empty(nr * per * L, dtype=torch.uint8, device=ctx.dev)
+    mo = torch.empty(nr * per + 1, dtype=torch.int64, device=ctx.dev)
+    n, nu, kb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+
+    def merge(evs):
+        call("vbf_compact_merge_dev", vp(keys), vp(offs), vp(created), vp(tomb), run_off.ctypes.data, nr,
+             None, None, None, 0, 0, 0, 10**15, 1 << 41, vp(ids), ctypes.byref(n), None, None,
+             ctypes.byref(nu), ctx.sp)
+
+    mwall, _, mph = timed_steps(ctx, merge, args.steps, args.warmup)
+    bf = vbf.BloomFilter(1e-4, max(n.value, 1), device=ctx.local)
+
+    def full(evs):
+        merge(evs)
+        call("vbf_gather_entries_dev", vp(keys), vp(offs), None, None, None, vp(ids), n.value, vp(mk), mk.numel(),
+             vp(mo), None, None, None, ctypes.byref(kb), ctx.sp)
+        bf.set_dev(vp(mk), None, L, n.value, 1, ctx.sp)
+
+    fwall, _, fph = timed_steps(ctx, full, args.steps, args.warmup)
+    total = nr * per
+    res = {"metric": "compaction merge entries/s (4 sorted tables -> merged table + its filter, device-resident)",
+           "value": ctx.sum_over_ranks(total) * args.steps / fwall, "unit": "entries/s", "n_gpus": ctx.world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": fwall / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+           "config": {"workload": "bucket of %d tables x %dM x 16B keys, %d merged entries" % (nr, per // 10**6, n.value)},
+           "merge_only": {"ms_per_step": mwall / args.steps * 1e3, "entries_per_s": total * args.steps / mwall,
+                          "phases": phase_report(mph, args.steps)},
+           "phases": phase_report(fph, args.steps)}
+    if ctx.world == 1 and ctx.rank == 0 and not args.no_cpu_baseline:
+        import oracle
+        ns = min(per, args.cpu_sample // nr)
+        hk = np.concatenate([k.view(-1, L)[:ns].cpu().numpy().reshape(-1) for k in ks])
+        ho = np.arange(nr * ns + 1, dtype=np.uint64) * L
+        hc = np.concatenate([c[:ns].cpu().numpy() for c in cr])
+        ht = np.concatenate([t[:ns].cpu().numpy() for t in tb])
+        t0 = time.perf_counter()
+        oracle.compact_merge(hk, ho, hc, ht, np.arange(nr + 1, dtype=np.uint64) * ns, False, 0, 10**15, 1 << 41)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": nr * ns / dt, "unit": "entries/s", "cores": 1, "kind": "port",
+                               "sample": "first %d entries of each table: the pairwise fold only" % ns,
+                               "seconds": round(dt, 3)}
+    return res
+
+
+def bench_multi(ctx, args):
+    """100M device-resident 16-byte keys probed against 8 SST filters (each
+    10M keys at 10 bits/key) in one launch -- key-range test + contains() per (key, SST)."""
+    n, L, S = args.keys, 16, 8
+    keys = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
+    call("vbf_gen_fixed_dev", wl.SEED_CFG2, 0, n, L, vp(keys), ctx.sp)
+    p = wl.fpr_for_bits_per_key(10)
+    filters = []
+    for s_ in range(S):
+        f = vbf.BloomFilter(p, 10_000_000, device=ctx.local)
+        f.set_dev(vp(keys[s_ * 10_000_000 * L:]), None, L, 10_000_000, 1, ctx.sp)
+        filters.append(f)
+    handles = (ctypes.c_void_p * S)(*[f._h.value for f in filters])
+    out = torch.empty(n * S, dtype=torch.uint8, device=ctx.dev)
+
+    def step(evs):
+        call("vbf_multi_probe_dev", vp(keys), None, L, n, 1, S, handles, None, None, vp(out), ctx.sp)
+
+    wall, _, _ = timed_steps(ctx, step, args.steps, args.warmup)
+    hits = int(out.view(n, S).any(dim=1).sum().item())
+    return {"metric": "multi-SST probe keys/s (each key tested against 8 filters, device-resident)",
+            "value": ctx.sum_over_ranks(n) * args.steps / wall, "unit": "keys/s", "n_gpus": ctx.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "%dM x 16B keys vs %d filters of 10M keys (m=1e8, k=10); %d keys hit some SST"
+                       % (n // 10**6, S, hits)},
+            "probes_per_s": ctx.sum_over_ranks(n) * S * args.steps / wall}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -410,6 +503,8 @@ def main():
     ap.add_argument("--neg-keys", type=int, default=None)
     ap.add_argument("--e2e", action="store_true")
     ap.add_argument("--sst", action="store_true", help="SST data.db decode + rebuild (8(f) row 2)")
+    ap.add_argument("--compact", action="store_true", help="compaction merge + filter (8(f) row 3)")
+    ap.add_argument("--multi", action="store_true", help="batched multi-SST probe (8(f) row 4)")
     ap.add_argument("--strategy", type=int, default=0, help="0 auto, 1 atomic, 2 partitioned")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
@@ -424,6 +519,12 @@ def main():
         args.keys = args.keys or 100_000_000
         args.neg_keys = args.neg_keys or 50_000_000
         res = bench_var(ctx, args)
+    elif args.compact:
+        args.keys = args.keys or 100_000_000
+        res = bench_compact(ctx, args)
+    elif args.multi:
+        args.keys = args.keys or 100_000_000
+        res = bench_multi(ctx, args)
     elif args.sst:
         args.keys = args.keys or 100_000_000
         res = bench_sst(ctx, args)

@@ -61,7 +61,7 @@ int vbf_device_count(int* count);
 
 /* Kernel-phase timing with hipEvents on the launch streams (for bench.py's roofline):
  * phases 0 tile-sort, 1 transpose, 2 segment-OR (partitioned build), 3 atomic build, 4 probe,
- * 5 data.db walk, 6 data.db scan, 7 data.db emit.
+ * 5 data.db walk, 6 data.db scan, 7 data.db emit, 8 compaction merge levels, 9 fold, 10 select.
  * vbf_profile_read synchronizes, returns per-phase summed ms and launch counts, and resets. */
 int vbf_profile_enable(int on);
 int vbf_profile_read(double* ms, uint64_t* launches, int nphases);

@@ -35,6 +35,8 @@ for s in $STEPS; do
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
     bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;
     sst)    run bench_sst 600 python bench.py --sst --steps 5 --warmup 1 ;;
+    compact) run bench_compact 600 python bench.py --compact --steps 5 --warmup 1 ;;
+    multi)  run bench_multi 600 python bench.py --multi --steps 5 --warmup 1 ;;
     e2e)    run bench_e2e 600 python bench.py --e2e --steps 3 --warmup 1 ;;
     ubench) run ubench 300 ./tools/ubench ;;
     counters) (cd /tmp && run counters 120 rocprofv3 -L) || exit $? ;;

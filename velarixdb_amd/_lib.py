@@ -128,7 +128,8 @@ def device_count():
     return c.value if rc == VBF_OK else 0
 
 
-PHASES = ("tile_sort", "transpose", "seg_or", "atomic_build", "probe", "sst_walk", "sst_scan", "sst_emit")
+PHASES = ("tile_sort", "transpose", "seg_or", "atomic_build", "probe", "sst_walk", "sst_scan", "sst_emit",
+          "merge_levels", "fold", "select")
 
 
 def profile_read():

@@ -1233,14 +1233,25 @@ int compact_merge(const uint8_t* keys, const uint64_t* offsets, const int64_t* c
     if (total && (!offsets || !created || !tomb || !out_ids)) return fail(VBF_EINVAL, "NULL argument");
     if (map_n && (!map_keys || !map_off || !map_time)) return fail(VBF_EINVAL, "map arrays are NULL");
     if (total == 0) return VBF_OK;
-    // merge levels: segment boundaries per level, all uploaded at once
+    // merge levels: segment boundaries and per-pair tile starts per level, all uploaded at once
+    const uint64_t tile = vbf::compact_tile();
     std::vector<uint64_t> bnd(run_off, run_off + nruns + 1);
-    std::vector<uint64_t> all;
+    std::vector<uint64_t> all, tiles_all, ntiles_lv;
     std::vector<uint32_t> nseg_lv;
+    uint64_t max_tiles = 1;
     uint32_t nseg = nruns;
     while (nseg > 1) {
         all.insert(all.end(), bnd.begin(), bnd.end());
         nseg_lv.push_back(nseg);
+        uint64_t t = 0;
+        for (uint32_t i = 0; i < nseg; i += 2) {
+            tiles_all.push_back(t);
+            const uint64_t len = bnd[std::min(i + 2, nseg)] - bnd[i];
+            t += (len + tile - 1) / tile;
+        }
+        tiles_all.push_back(t);
+        ntiles_lv.push_back(t);
+        max_tiles = std::max(max_tiles, t);
         std::vector<uint64_t> nb;
         for (uint32_t i = 0; i < nseg; i += 2) nb.push_back(bnd[i]);
         nb.push_back(bnd[nseg]);
@@ -1254,7 +1265,9 @@ int compact_merge(const uint8_t* keys, const uint64_t* offsets, const int64_t* c
     const uint64_t o_pong = align256(total * 4), o_keep = o_pong + align256(total * 4);
     const uint64_t o_sel = o_keep + align256(total), o_upd = o_sel + align256(total * 4);
     const uint64_t o_ut = o_upd + align256(total), o_ro = o_ut + align256(total * 8);
-    const uint64_t o_bnd = o_ro + align256((nruns + 1) * 8), o_misc = o_bnd + align256(all.size() * 8 + 8);
+    const uint64_t o_bnd = o_ro + align256((nruns + 1) * 8), o_tl = o_bnd + align256(all.size() * 8 + 8);
+    const uint64_t o_pp = o_tl + align256(tiles_all.size() * 8 + 8), o_pq = o_pp + align256(total * 8);
+    const uint64_t o_split = o_pq + align256(total * 8), o_misc = o_split + align256(max_tiles * 8);
     const uint64_t o_tmp = o_misc + 256, bytes = o_tmp + t3;
     void* ws = nullptr;
     int rc = get_workspace(s, bytes, &ws, kWsCompact);
@@ -1268,18 +1281,30 @@ int compact_merge(const uint8_t* keys, const uint64_t* offsets, const int64_t* c
     int64_t* ut = reinterpret_cast<int64_t*>(b + o_ut);
     uint64_t* d_ro = reinterpret_cast<uint64_t*>(b + o_ro);
     uint64_t* d_bnd = reinterpret_cast<uint64_t*>(b + o_bnd);
+    uint64_t* d_tl = reinterpret_cast<uint64_t*>(b + o_tl);
+    uint64_t* pping = reinterpret_cast<uint64_t*>(b + o_pp);
+    uint64_t* ppong = reinterpret_cast<uint64_t*>(b + o_pq);
+    uint64_t* split = reinterpret_cast<uint64_t*>(b + o_split);
     uint64_t* misc = reinterpret_cast<uint64_t*>(b + o_misc);  // [0] n_out, [1] n_upd, [2] sort error
     HIP_TRY(hipMemcpyAsync(d_ro, run_off, (nruns + 1) * 8, hipMemcpyHostToDevice, s));
     if (!all.empty()) HIP_TRY(hipMemcpyAsync(d_bnd, all.data(), all.size() * 8, hipMemcpyHostToDevice, s));
+    if (!tiles_all.empty())
+        HIP_TRY(hipMemcpyAsync(d_tl, tiles_all.data(), tiles_all.size() * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(misc, 0, 16, s));
     HIP_TRY(hipMemsetAsync(misc + 2, 0xFF, 8, s));
     vbf::CompactArgs a{keys, offsets, created, tomb, d_ro, nruns, map_keys, map_off, map_time, map_n, use_ttl,
                        entry_ttl_ms, tomb_ttl_ms, now_ms, total};
+    vbf::phase_begin(vbf::kPhaseMergeLevels, s);
     HIP_TRY(vbf::compact_check_sorted(a, reinterpret_cast<uint32_t*>(misc + 2), s));
-    HIP_TRY(vbf::launch_iota_u32(ping, total, s));
     uint32_t* order = nullptr;
-    HIP_TRY(vbf::compact_merge_levels(a, d_bnd, nseg_lv.data(), (uint32_t)nseg_lv.size(), ping, pong, &order, s));
-    HIP_TRY(vbf::compact_fold(a, order, total, keep, sel, upd, ut, s));
+    uint64_t* opfx = nullptr;
+    HIP_TRY(vbf::compact_merge_levels(a, d_bnd, d_tl, nseg_lv.data(), ntiles_lv.data(), (uint32_t)nseg_lv.size(),
+                                      ping, pong, pping, ppong, split, &order, &opfx, s));
+    vbf::phase_end(vbf::kPhaseMergeLevels, s);
+    vbf::phase_begin(vbf::kPhaseFold, s);
+    HIP_TRY(vbf::compact_fold(a, order, opfx, total, keep, sel, upd, ut, s));
+    vbf::phase_end(vbf::kPhaseFold, s);
+    vbf::phase_begin(vbf::kPhaseSelect, s);
     size_t tb = t3;
     HIP_TRY(vbf::select_u32(b + o_tmp, &tb, sel, keep, out_ids, misc, total, s));
     if (upd_ids && upd_time) {
@@ -1288,6 +1313,7 @@ int compact_merge(const uint8_t* keys, const uint64_t* offsets, const int64_t* c
         tb = t3;
         HIP_TRY(vbf::select_i64(b + o_tmp, &tb, ut, upd, upd_time, misc + 1, total, s));
     }
+    vbf::phase_end(vbf::kPhaseSelect, s);
     uint64_t hv[3];
     HIP_TRY(hipMemcpyAsync(hv, misc, 24, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));

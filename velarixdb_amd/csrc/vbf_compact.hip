@@ -30,10 +30,21 @@ namespace vbf {
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kMergeIpt = 4;  // outputs per lane per merge level
 
-// Rust `Ord for [u8]` on two keys of the arena.
+// Rust `Ord for [u8]` on two keys of the arena: 8 bytes at a time as big-endian words (global
+// memory takes unaligned 8-byte loads), then the tail byte by byte.
+__device__ __forceinline__ uint64_t ld_be64(const uint8_t* p) {
+    uint64_t w;
+    __builtin_memcpy(&w, p, 8);
+    return __builtin_bswap64(w);
+}
+
 __device__ __forceinline__ int cmp_keys(const uint8_t* ka, uint64_t la, const uint8_t* kb, uint64_t lb) {
     const uint64_t n = la < lb ? la : lb;
     uint64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const uint64_t x = ld_be64(ka + i), y = ld_be64(kb + i);
+        if (x != y) return x < y ? -1 : 1;
+    }
     for (; i < n; ++i) {
         const uint32_t x = ka[i], y = kb[i];
         if (x != y) return x < y ? -1 : 1;
@@ -46,39 +57,117 @@ __device__ __forceinline__ int cmp_ids(const CompactArgs& a, uint32_t x, uint32_
     return cmp_keys(a.keys + bx, a.offsets[x + 1] - bx, a.keys + by, a.offsets[y + 1] - by);
 }
 
-// One merge level: segments [bnd[s], bnd[s+1]) of `in`, pairs (2p, 2p+1) merged into `out`
-// (an unpaired last segment is copied).  Stable: on equal keys the left (earlier) side first.
-__global__ __launch_bounds__(256) void k_merge_level(CompactArgs a, const uint64_t* bnd, uint32_t nseg,
-                                                     const uint32_t* in, uint32_t* out) {
-    const uint64_t total = bnd[nseg] - bnd[0];
-    uint64_t o = bnd[0] + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kMergeIpt;
-    if (o >= bnd[0] + total) return;
-    const uint64_t o_end = std::min<uint64_t>(o + kMergeIpt, bnd[0] + total);
-    // pair containing o: largest even s with bnd[s] <= o
-    uint32_t lo = 0, hi = (nseg - 1) / 2;
+// Big-endian 8-byte prefix of a key (zero-padded): prefixes order keys except on ties.
+__device__ __forceinline__ uint64_t key_prefix8(const uint8_t* k, uint64_t len) {
+    if (len >= 8) return ld_be64(k);
+    uint64_t w = 0;
+    for (uint64_t i = 0; i < len; ++i) w |= (uint64_t)k[i] << (56 - 8 * i);
+    return w;
+}
+
+__global__ __launch_bounds__(256) void k_prefixes(CompactArgs a, uint32_t* ids, uint64_t* pfx) {
+    const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= a.run_off_host_total) return;
+    const uint64_t b = a.offsets[e];
+    ids[e] = (uint32_t)e;
+    pfx[e] = key_prefix8(a.keys + b, a.offsets[e + 1] - b);
+}
+
+// (prefix, id) order: prefixes first, the full keys only on a prefix tie.
+__device__ __forceinline__ int cmp_pid(const CompactArgs& a, uint64_t px, uint32_t x, uint64_t py, uint32_t y) {
+    if (px != py) return px < py ? -1 : 1;
+    return cmp_ids(a, x, y);
+}
+
+// Merge levels, two-level merge path.  Pairs (2p, 2p+1) of segments [bnd[s], bnd[s+1]) are cut
+// into tiles of kTile outputs; k_merge_split finds every tile's start on its merge path (one
+// binary search per tile, over the carried prefixes), k_merge_tile stages the tile's two input
+// ranges (ids + prefixes) in LDS and merges them there, 8 outputs per lane.  Stable: on equal
+// keys the left (earlier-table) side first.
+constexpr uint32_t kTile = 2048;
+constexpr uint32_t kTileIpt = kTile / 256;
+
+struct LevelGeom {
+    const uint64_t* bnd;       // nseg + 1 segment boundaries
+    const uint64_t* tile_base; // npairs + 1: first tile of each pair
+    uint32_t nseg, npairs;
+    uint64_t ntiles;
+};
+
+__device__ __forceinline__ void tile_pair(const LevelGeom& g, uint64_t t, uint32_t& p, uint64_t& a0, uint64_t& a1,
+                                          uint64_t& b1) {
+    uint32_t lo = 0, hi = g.npairs - 1;  // last pair whose first tile <= t
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) / 2;
-        if (bnd[2 * mid] <= o) lo = mid;
+        if (g.tile_base[mid] <= t) lo = mid;
         else hi = mid - 1;
     }
-    uint32_t p = lo;
-    while (o < o_end) {
-        const uint64_t a0 = bnd[2 * p], a1 = bnd[std::min(2 * p + 1, nseg)], b1 = bnd[std::min(2 * p + 2, nseg)];
-        const uint64_t na = a1 - a0, nb = b1 - a1, d = o - a0;
-        // merge path: i = number of A items among the first d outputs
-        uint64_t l = d > nb ? d - nb : 0, h = d < na ? d : na;
-        while (l < h) {
-            const uint64_t mid = (l + h) / 2;
-            if (cmp_ids(a, in[a0 + mid], in[a1 + d - 1 - mid]) <= 0) l = mid + 1;
-            else h = mid;
-        }
-        uint64_t i = l, j = d - l;
-        const uint64_t stop = std::min(o_end, b1);
-        for (; o < stop; ++o) {
-            if (j >= nb || (i < na && cmp_ids(a, in[a0 + i], in[a1 + j]) <= 0)) out[o] = in[a0 + i++];
-            else out[o] = in[a1 + j++];
-        }
-        ++p;
+    p = lo;
+    a0 = g.bnd[2 * p];
+    a1 = g.bnd[std::min(2 * p + 1, g.nseg)];
+    b1 = g.bnd[std::min(2 * p + 2, g.nseg)];
+}
+
+// split[t] = number of A items among the first d outputs of tile t's pair (d = tile start).
+__global__ __launch_bounds__(256) void k_merge_split(CompactArgs a, LevelGeom g, const uint32_t* in,
+                                                     const uint64_t* pin, uint64_t* split) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= g.ntiles) return;
+    uint32_t p;
+    uint64_t a0, a1, b1;
+    tile_pair(g, t, p, a0, a1, b1);
+    const uint64_t na = a1 - a0, nb = b1 - a1, d = (t - g.tile_base[p]) * kTile;
+    uint64_t l = d > nb ? d - nb : 0, h = d < na ? d : na;
+    while (l < h) {
+        const uint64_t mid = (l + h) / 2;
+        const uint64_t y = a1 + d - 1 - mid;
+        if (cmp_pid(a, pin[a0 + mid], in[a0 + mid], pin[y], in[y]) <= 0) l = mid + 1;
+        else h = mid;
+    }
+    split[t] = l;
+}
+
+__global__ __launch_bounds__(256) void k_merge_tile(CompactArgs a, LevelGeom g, const uint32_t* in,
+                                                    const uint64_t* pin, const uint64_t* split, uint32_t* out,
+                                                    uint64_t* pout) {
+    __shared__ uint64_t sp[kTile];
+    __shared__ uint32_t si[kTile];
+    const uint64_t t = blockIdx.x;
+    uint32_t p;
+    uint64_t a0, a1, b1;
+    tile_pair(g, t, p, a0, a1, b1);
+    const uint64_t na = a1 - a0, nb = b1 - a1, n = na + nb;
+    const uint64_t d0 = (t - g.tile_base[p]) * kTile, d1 = std::min<uint64_t>(d0 + kTile, n);
+    const uint64_t i0 = split[t], j0 = d0 - i0;
+    const uint64_t i1 = (t + 1 < g.tile_base[p + 1]) ? split[t + 1] : na, j1 = d1 - i1;
+    const uint32_t la = (uint32_t)(i1 - i0), lb = (uint32_t)(j1 - j0);  // la + lb = d1 - d0
+    for (uint32_t x = threadIdx.x; x < la + lb; x += 256) {
+        const uint64_t src = x < la ? a0 + i0 + x : a1 + j0 + (x - la);
+        si[x] = in[src];
+        sp[x] = pin[src];
+    }
+    __syncthreads();
+    // this lane's outputs [dt, dt + kTileIpt) of the tile: its own merge path in LDS
+    const uint32_t dt = threadIdx.x * kTileIpt, tot = la + lb;
+    if (dt >= tot) return;
+    uint32_t l = dt > lb ? dt - lb : 0, h = dt < la ? dt : la;
+    while (l < h) {
+        const uint32_t mid = (l + h) / 2;
+        const uint32_t y = la + dt - 1 - mid;
+        if (cmp_pid(a, sp[mid], si[mid], sp[y], si[y]) <= 0) l = mid + 1;
+        else h = mid;
+    }
+    uint32_t i = l, j = dt - l;
+    const uint32_t stop = std::min(dt + kTileIpt, tot);
+    const uint64_t ob = a0 + d0;
+    for (uint32_t o = dt; o < stop; ++o) {
+        bool take_a;
+        if (j >= lb) take_a = true;
+        else if (i >= la) take_a = false;
+        else take_a = cmp_pid(a, sp[i], si[i], sp[la + j], si[la + j]) <= 0;
+        const uint32_t x = take_a ? i++ : la + j++;
+        out[ob + o] = si[x];
+        pout[ob + o] = sp[x];
     }
 }
 
@@ -93,16 +182,18 @@ __device__ __forceinline__ uint32_t run_of(const CompactArgs& a, uint32_t id) {
 }
 
 // One lane per position; lanes at the first entry of a key replay that key's fold.
-__global__ __launch_bounds__(256) void k_fold(CompactArgs a, const uint32_t* order, uint64_t total, uint8_t* keep,
-                                              uint32_t* sel, uint8_t* upd, int64_t* upd_time) {
+__global__ __launch_bounds__(256) void k_fold(CompactArgs a, const uint32_t* order, const uint64_t* opfx,
+                                              uint64_t total, uint8_t* keep, uint32_t* sel, uint8_t* upd,
+                                              int64_t* upd_time) {
     const uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= total) return;
     keep[p] = 0;
     upd[p] = 0;
     const uint32_t first = order[p];
-    if (p > 0 && cmp_ids(a, order[p - 1], first) == 0) return;  // not the key's first entry
+    const uint64_t fp = opfx[p];
+    if (p > 0 && cmp_pid(a, opfx[p - 1], order[p - 1], fp, first) == 0) return;  // not the key's first entry
     uint64_t q = p + 1;
-    while (q < total && cmp_ids(a, first, order[q]) == 0) ++q;  // group [p, q): one per table
+    while (q < total && cmp_pid(a, fp, first, opfx[q], order[q]) == 0) ++q;  // group [p, q): one per table
     const uint8_t* kp = a.keys + a.offsets[first];
     const uint64_t kl = a.offsets[first + 1] - a.offsets[first];
 
@@ -213,29 +304,44 @@ hipError_t compact_check_sorted(const CompactArgs& a, uint32_t* err, hipStream_t
     return hipGetLastError();
 }
 
-hipError_t compact_merge_levels(const CompactArgs& a, const uint64_t* d_bnd_all, const uint32_t* nseg_per_level,
-                                uint32_t nlevels, uint32_t* ping, uint32_t* pong, uint32_t** result, hipStream_t s) {
+hipError_t compact_merge_levels(const CompactArgs& a, const uint64_t* d_bnd_all, const uint64_t* d_tiles_all,
+                                const uint32_t* nseg_per_level, const uint64_t* ntiles_per_level, uint32_t nlevels,
+                                uint32_t* ping, uint32_t* pong, uint64_t* pping, uint64_t* ppong, uint64_t* split,
+                                uint32_t** result, uint64_t** presult, hipStream_t s) {
     const uint64_t total = a.run_off_host_total;
+    hipLaunchKernelGGL(k_prefixes, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, a, ping, pping);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     uint32_t* in = ping;
     uint32_t* out = pong;
+    uint64_t* pin = pping;
+    uint64_t* pout = ppong;
     const uint64_t* bnd = d_bnd_all;
-    const uint64_t grid = (total + 256 * kMergeIpt - 1) / (256 * kMergeIpt);
+    const uint64_t* tb = d_tiles_all;
     for (uint32_t l = 0; l < nlevels; ++l) {
-        const uint32_t nseg = nseg_per_level[l];
-        hipLaunchKernelGGL(k_merge_level, dim3((uint32_t)grid), dim3(256), 0, s, a, bnd, nseg, in, out);
-        hipError_t e = hipGetLastError();
+        const uint32_t nseg = nseg_per_level[l], npairs = (nseg + 1) / 2;
+        const LevelGeom g{bnd, tb, nseg, npairs, ntiles_per_level[l]};
+        hipLaunchKernelGGL(k_merge_split, dim3((uint32_t)((g.ntiles + 255) / 256)), dim3(256), 0, s, a, g, in, pin,
+                           split);
+        hipLaunchKernelGGL(k_merge_tile, dim3((uint32_t)g.ntiles), dim3(256), 0, s, a, g, in, pin, split, out, pout);
+        e = hipGetLastError();
         if (e != hipSuccess) return e;
         bnd += nseg + 1;
+        tb += npairs + 1;
         std::swap(in, out);
+        std::swap(pin, pout);
     }
     *result = in;
+    *presult = pin;
     return hipSuccess;
 }
 
-hipError_t compact_fold(const CompactArgs& a, const uint32_t* order, uint64_t total, uint8_t* keep, uint32_t* sel,
-                        uint8_t* upd, int64_t* upd_time, hipStream_t s) {
-    hipLaunchKernelGGL(k_fold, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, a, order, total, keep, sel, upd,
-                       upd_time);
+uint32_t compact_tile() { return kTile; }
+
+hipError_t compact_fold(const CompactArgs& a, const uint32_t* order, const uint64_t* opfx, uint64_t total,
+                        uint8_t* keep, uint32_t* sel, uint8_t* upd, int64_t* upd_time, hipStream_t s) {
+    hipLaunchKernelGGL(k_fold, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, a, order, opfx, total, keep,
+                       sel, upd, upd_time);
     return hipGetLastError();
 }
 

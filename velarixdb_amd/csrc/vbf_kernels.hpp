@@ -21,7 +21,8 @@ hipError_t launch_build(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* wo
 
 // Optional per-phase timing (vbf_profile_*): HIP events recorded on the launch stream.
 enum Phase { kPhaseTileSort = 0, kPhaseTranspose = 1, kPhaseSegOr = 2, kPhaseAtomicBuild = 3,
-             kPhaseProbe = 4, kPhaseSstWalk = 5, kPhaseSstScan = 6, kPhaseSstEmit = 7, kNumPhases = 8 };
+             kPhaseProbe = 4, kPhaseSstWalk = 5, kPhaseSstScan = 6, kPhaseSstEmit = 7,
+             kPhaseMergeLevels = 8, kPhaseFold = 9, kPhaseSelect = 10, kNumPhases = 11 };
 void phase_begin(int phase, hipStream_t s);
 void phase_end(int phase, hipStream_t s);
 
@@ -121,10 +122,13 @@ struct GatherArgs {
 };
 hipError_t launch_iota_u32(uint32_t* out, uint64_t n, hipStream_t s);
 hipError_t compact_check_sorted(const CompactArgs& a, uint32_t* err, hipStream_t s);
-hipError_t compact_merge_levels(const CompactArgs& a, const uint64_t* d_bnd_all, const uint32_t* nseg_per_level,
-                                uint32_t nlevels, uint32_t* ping, uint32_t* pong, uint32_t** result, hipStream_t s);
-hipError_t compact_fold(const CompactArgs& a, const uint32_t* order, uint64_t total, uint8_t* keep, uint32_t* sel,
-                        uint8_t* upd, int64_t* upd_time, hipStream_t s);
+hipError_t compact_merge_levels(const CompactArgs& a, const uint64_t* d_bnd_all, const uint64_t* d_tiles_all,
+                                const uint32_t* nseg_per_level, const uint64_t* ntiles_per_level, uint32_t nlevels,
+                                uint32_t* ping, uint32_t* pong, uint64_t* pping, uint64_t* ppong, uint64_t* split,
+                                uint32_t** result, uint64_t** presult, hipStream_t s);
+uint32_t compact_tile();
+hipError_t compact_fold(const CompactArgs& a, const uint32_t* order, const uint64_t* opfx, uint64_t total,
+                        uint8_t* keep, uint32_t* sel, uint8_t* upd, int64_t* upd_time, hipStream_t s);
 hipError_t select_u32(void* tmp, size_t* bytes, const uint32_t* in, const uint8_t* flags, uint32_t* out,
                       uint64_t* nsel, uint64_t n, hipStream_t s);
 hipError_t select_i64(void* tmp, size_t* bytes, const int64_t* in, const uint8_t* flags, int64_t* out,
