@@ -213,6 +213,31 @@ __global__ __launch_bounds__(1024) void k_lds(int n, uint32_t* out) {
     if (acc == 0xdeadbeef || a[threadIdx.x] == 0xdeadbeef) out[0] = acc;
 }
 
+// Segment-major reservation: each of ntiles workgroups reserves room for its runs in nseg
+// per-segment cursors (one returning atomicAdd per segment per tile).
+__global__ __launch_bounds__(1024) void k_reserve(uint32_t* cur, uint32_t nseg, uint32_t* out) {
+    uint32_t acc = 0;
+    for (uint32_t s = threadIdx.x; s < nseg; s += 1024) acc += atomicAdd(&cur[s], 32u + (s & 7));
+    if (acc == 0xdeadbeef) out[0] = acc;
+}
+
+// Scatter of the tile runs to segment-major slots: 8-lane groups write 80-byte runs.
+__global__ __launch_bounds__(1024) void k_scatter(uint4* dst, uint32_t nseg, uint32_t ntiles, uint32_t slot16) {
+    const uint32_t t = blockIdx.x, grp = threadIdx.x >> 3, q = threadIdx.x & 7;
+    for (uint32_t s = grp; s < nseg; s += 128)
+        if (q < 5) dst[((uint64_t)s * ntiles + t) * slot16 + q] = make_uint4(t, s, q, 1);
+}
+
+// Stream read of n16 uint4 (one pass, grid-stride).
+__global__ __launch_bounds__(256) void k_stream(const uint4* src, uint64_t n16, uint32_t* out) {
+    uint32_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) {
+        const uint4 v = src[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0xdeadbeef) out[0] = acc;
+}
+
 template <class F>
 static float time_ms(F&& f, int reps) {
     hipEvent_t a, b;
@@ -291,6 +316,27 @@ int main() {
         run(k_lds<2>, "ds_write_b32");
         run(k_lds<3>, "ds_write_b16");
         run(k_lds<4>, "ds_or_b32, half lanes or 0");
+    }
+    {
+        uint32_t *cur, *o;
+        CHECK(hipMalloc(&cur, 4096 * 4));
+        CHECK(hipMalloc(&o, 4));
+        CHECK(hipMemset(cur, 0, 4096 * 4));
+        const uint32_t ntiles = 33058, nseg = 954;
+        float t = time_ms([&] { hipLaunchKernelGGL(k_reserve, dim3(ntiles), dim3(1024), 0, 0, cur, nseg, o); }, 3);
+        printf("segment reservation: %u tiles x %u returning atomicAdds on %u cursors: %.3f ms (%.2f G atomics/s)\n",
+               ntiles, nseg, nseg, t, (double)ntiles * nseg / t / 1e6);
+        uint4* big;
+        const uint64_t slot16 = 8;  // 128-byte slots
+        const uint64_t bytes = (uint64_t)ntiles * nseg * slot16 * 16;
+        CHECK(hipMalloc(&big, bytes));
+        float ts = time_ms([&] { hipLaunchKernelGGL(k_scatter, dim3(ntiles), dim3(1024), 0, 0, big, nseg, ntiles, (uint32_t)slot16); }, 3);
+        printf("scatter of 80-byte runs into 128-byte segment-major slots (%.2f GB written): %.3f ms (%.1f GB/s)\n",
+               (double)ntiles * nseg * 80 / 1e9, ts, (double)ntiles * nseg * 80 / ts / 1e6);
+        const uint64_t n16 = (2600ull << 20) / 16;
+        float tr = time_ms([&] { hipLaunchKernelGGL(k_stream, dim3(256 * 16), dim3(256), 0, 0, big, n16, o); }, 3);
+        printf("stream read 2.6 GiB: %.3f ms (%.1f GB/s)\n", tr, (double)n16 * 16 / tr / 1e6);
+        CHECK(hipFree(big));
     }
     uint32_t* w;
     const uint64_t maxw = 1ull << 29;  // 2 GiB
