@@ -112,6 +112,20 @@ def timed_steps(ctx, step, steps, warmup):
     return ctx.max_over_ranks(t1 - t0), kms, phases
 
 
+def time_probe_strategies(ctx, launch, reps=3):
+    """Mean ms of one probe call per strategy (2 partitioned, 1 per-key gather), after a warm-up."""
+    res = {}
+    for strat, name in ((2, "partitioned"), (1, "gather")):
+        launch(strat)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            launch(strat)
+        torch.cuda.synchronize()
+        res[name] = (time.perf_counter() - t0) / reps * 1e3
+    return res
+
+
 def phase_report(phases, steps):
     return {p: {"ms_per_launch": ms / n, "launches": n} for p, (ms, n) in phases.items() if n}
 
@@ -160,6 +174,8 @@ def bench_fixed(ctx, args):
     call("vbf_popcount_dev", vp(words), nwords, vp(pop), ctx.sp)
     torch.cuda.synchronize()
     assert int(cnt.item()) == n, "false negatives: %d of %d keys found" % (cnt.item(), n)
+    sweep = time_probe_strategies(ctx, lambda st: call("vbf_probe_count_dev_ex", vp(keys), None, L, n, 1, m, k,
+                                                       vp(words), vp(cnt), st, ctx.sp))
 
     total_keys = ctx.sum_over_ranks(n) * args.steps
     value = total_keys / wall
@@ -187,6 +203,7 @@ def bench_fixed(ctx, args):
                      "siprounds_per_key": (L + 8) // 8 + 5 * k,
                      "phases": phase_report(phases, args.steps)},
         "fill_ratio": int(pop.item()) / m,
+        "positive_sweep_ms": sweep,
     }
     if ctx.world == 1 and ctx.rank == 0 and not args.no_cpu_baseline:
         ns = args.cpu_sample
@@ -256,10 +273,13 @@ def bench_var(ctx, args):
         "config": {"workload": "config3: %dM var-length keys (Zipf 8..128 B, mean %.1f B), %d bits/key (m=%d, k=%d) + %dM negative probes"
                    % (n // 10**6, mean_len, args.bits_per_key, m, k, nn // 10**6)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_generic<Build,offsets>",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "partitioned build (offsets layout)",
                      "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_key": bpk},
         "probe": {"keys_per_s": nn / (float(np.mean(pkms)) / 1e3), "false_positives": fp,
-                  "fpr": fp / nn, "kernel_ms": float(np.mean(pkms))},
+                  "fpr": fp / nn, "kernel_ms": float(np.mean(pkms)),
+                  "ms_by_strategy": time_probe_strategies(ctx, lambda st: call(
+                      "vbf_probe_count_dev_ex", vp(nkeys), vp(noff), 0, nn, 1, m, k, vp(words), vp(cnt), st,
+                      ctx.sp))},
     }
 
 

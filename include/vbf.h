@@ -61,7 +61,8 @@ int vbf_device_count(int* count);
 
 /* Kernel-phase timing with hipEvents on the launch streams (for bench.py's roofline):
  * phases 0 tile-sort, 1 transpose, 2 segment-OR (partitioned build), 3 atomic build, 4 probe,
- * 5 data.db walk, 6 data.db scan, 7 data.db emit, 8 compaction merge levels, 9 fold, 10 select.
+ * 5 data.db walk, 6 data.db scan, 7 data.db emit, 8 compaction merge levels, 9 fold, 10 select,
+ * 11 partitioned-probe pack, 12 probe segment test, 13 probe answers.
  * vbf_profile_read synchronizes, returns per-phase summed ms and launch counts, and resets. */
 int vbf_profile_enable(int on);
 int vbf_profile_read(double* ms, uint64_t* launches, int nphases);
@@ -104,6 +105,21 @@ int vbf_release_workspaces(void);
 int vbf_probe_count_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                         int len_prefix, uint32_t m, uint32_t k, const uint32_t* words,
                         unsigned long long* count_dev, void* stream);
+
+/* Same with an explicit strategy: VBF_BUILD_ATOMIC (one lane per key, early exit on the first
+ * clear bit, random filter loads), VBF_BUILD_PARTITIONED (keys hashed in tiles, entries sorted by
+ * 2^20-bit filter segment, every bit test against a segment staged in LDS; all k hashes per key),
+ * VBF_BUILD_AUTO (the calls above): for batches of >= 2^24 bit tests against filters of >= 2^26
+ * bits it probes the first 65 536 keys by gather, reads their hit count back (one stream
+ * synchronisation) and goes partitioned when >= 35 % hit (positive sweeps), gather otherwise.
+ * Identical answers either way. */
+int vbf_probe_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                     int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                     int strategy, void* stream);
+int vbf_probe_count_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                           uint64_t n, int len_prefix, uint32_t m, uint32_t k,
+                           const uint32_t* words, unsigned long long* count_dev, int strategy,
+                           void* stream);
 /* out[j*k + i] = calculate_hash(key_j, i) (bf.rs:222-227). */
 int vbf_hashes_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                    int len_prefix, uint32_t k, uint64_t* out, void* stream);

@@ -31,6 +31,7 @@ for s in $STEPS; do
     benchstagger14) run bench_stagger14 300 env VBF_STAGGER=14 python bench.py --no-cpu-baseline ;;
     ablate) run ablate 300 python tools/ablate.py ;;
     ablatesst) run ablate_sst 300 python tools/ablate_sst.py ;;
+    probephases) run probe_phases 300 python tools/probe_phases.py ;;
     benchatomic) run bench_atomic 300 python bench.py --no-cpu-baseline --strategy 1 --steps 3 ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
     bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;

@@ -1,0 +1,90 @@
+"""GPU parity for the partitioned probe (contains(), bf.rs:95-105, for large batches): its
+answers equal the per-key early-exit probe and the oracle, bit for bit, across key layouts,
+filter sizes (one segment, a few, thousands, the u32-saturated config-5 size) and k values
+(compile-time 4/10 and run-time k)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # (L or None for var-length, len_prefix, m, k, n)
+    (16, 1, 100_000_000, 10, 2_000_000),
+    (32, 1, 4_294_967_295, 4, 1_000_000),
+    (8, 0, 5_000_000, 7, 500_000),        # 5 segments -> several workgroups per segment
+    (None, 1, 300_000_000, 19, 400_000),  # variable-length keys, run-time k
+    (24, 1, 1 << 20, 3, 300_000),         # exactly one segment
+    (13, 1, 3_000_000_000, 3, 600_000),   # unaligned stride
+]
+
+
+def _keys(torch, L, n, seed):
+    from velarixdb_amd._lib import call
+    dev = torch.device("cuda:0")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    if L is None:
+        from velarixdb_amd.workloads import var_offsets
+        offs = torch.from_numpy(var_offsets(seed, 0, n).view(np.int64)).to(dev)
+        keys = torch.empty(int(offs[-1].item()), dtype=torch.uint8, device=dev)
+        call("vbf_gen_var_dev", seed, 0, n, P(offs), P(keys), None)
+        return keys, offs, 0
+    keys = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    call("vbf_gen_fixed_dev", seed, 0, n, L, P(keys), None)
+    return keys, None, L
+
+
+@pytest.mark.parametrize("L,lp,m,k,n", CASES)
+def test_partitioned_probe_matches_gather_probe(vbf, ora, L, lp, m, k, n):
+    import torch
+    from velarixdb_amd._lib import call
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    keys, offs, stride = _keys(torch, L, n, 0x5EED0101)
+    words = torch.zeros((m + 31) // 32, dtype=torch.int32, device="cuda:0")
+    half = n // 2  # build from the first half: probes see positives and negatives
+    call("vbf_build_dev_ex", P(keys), P(offs), stride, half, lp, m, k, P(words), 0, None)
+    outs = {}
+    for strat in (1, 2):
+        o = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        call("vbf_probe_dev_ex", P(keys), P(offs), stride, n, lp, m, k, P(words), P(o), strat, None)
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+        call("vbf_probe_count_dev_ex", P(keys), P(offs), stride, n, lp, m, k, P(words), P(cnt), strat, None)
+        torch.cuda.synchronize()
+        outs[strat] = o.cpu().numpy()
+        assert int(cnt.item()) == int(outs[strat].sum())
+    assert np.array_equal(outs[1], outs[2])
+    assert outs[2][:half].all()  # no false negatives
+    # oracle on a slice of the negatives (and a few positives)
+    sl = slice(half - 1000, half + 20000)
+    if offs is None:
+        hk = keys.cpu().numpy().reshape(n, L)[sl]
+        batch = vbf.pack_fixed(hk, lp)
+    else:
+        o_h = offs.cpu().numpy().view(np.uint64)
+        kb = keys.cpu().numpy()
+        lo, hi = int(o_h[sl.start]), int(o_h[sl.stop])
+        batch = vbf.pack_offsets(kb[lo:hi], o_h[sl.start:sl.stop + 1] - lo, lp)
+    wh = words.cpu().numpy().view(np.uint32)
+    assert np.array_equal(ora.probe(batch, m, k, wh).astype(np.uint8), outs[2][sl])
+
+
+def test_partitioned_probe_edges(vbf):
+    """n = 1, n not a multiple of the tile, k = 0 (always true), unsupported k falls back."""
+    import torch
+    from velarixdb_amd._lib import VbfError, call
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    keys, _, _ = _keys(torch, 16, 5000, 3)
+    m = 1 << 27
+    words = torch.zeros(m // 32, dtype=torch.int32, device="cuda:0")
+    call("vbf_build_dev_ex", P(keys), None, 16, 2500, 1, m, 10, P(words), 0, None)
+    for n in (1, 1849, 1851, 4999):
+        a = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        b = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        call("vbf_probe_dev_ex", P(keys), None, 16, n, 1, m, 10, P(words), P(a), 1, None)
+        call("vbf_probe_dev_ex", P(keys), None, 16, n, 1, m, 10, P(words), P(b), 2, None)
+        assert torch.equal(a, b)
+    o = torch.zeros(100, dtype=torch.uint8, device="cuda:0")
+    call("vbf_probe_dev_ex", P(keys), None, 16, 100, 1, m, 0, P(words), P(o), 0, None)
+    assert bool(o.all())
+    with pytest.raises(VbfError):
+        call("vbf_probe_dev_ex", P(keys), None, 16, 100, 1, m, 33, P(words), P(o), 2, None)

@@ -47,6 +47,8 @@ SIGNATURES = {
     "vbf_release_workspaces": (_int, []),
     "vbf_probe_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _vp]),
     "vbf_probe_count_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _vp]),
+    "vbf_probe_dev_ex": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _int, _vp]),
+    "vbf_probe_count_dev_ex": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _int, _vp]),
     "vbf_hashes_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp]),
     "vbf_or_words_dev": (_int, [_vp, _vp, _u64, _vp]),
     "vbf_popcount_dev": (_int, [_vp, _u64, _vp, _vp]),
@@ -129,7 +131,7 @@ def device_count():
 
 
 PHASES = ("tile_sort", "transpose", "seg_or", "atomic_build", "probe", "sst_walk", "sst_scan", "sst_emit",
-          "merge_levels", "fold", "select")
+          "merge_levels", "fold", "select", "probe_pack", "probe_seg", "probe_out")
 
 
 def profile_read():

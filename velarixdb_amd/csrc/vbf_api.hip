@@ -98,7 +98,19 @@ vbf::KeyBatch batch(const uint8_t* keys, const uint64_t* offsets, uint64_t off_b
 // Partitioned-build workspace: one grow-only buffer per (device, stream), so concurrent
 // builds on different streams never share scratch.
 // ---------------------------------------------------------------------------------------
-enum WsSlot { kWsBuild = 0, kWsSstScratch = 1, kWsSstKeys = 2, kWsSstInput = 3, kWsMulti = 4, kWsMultiKeys = 5, kWsCompact = 6, kWsCompactIn = 7, kWsGather = 8 };
+enum WsSlot {
+    kWsBuild = 0,
+    kWsSstScratch = 1,
+    kWsSstKeys = 2,
+    kWsSstInput = 3,
+    kWsMulti = 4,
+    kWsMultiKeys = 5,
+    kWsCompact = 6,
+    kWsCompactIn = 7,
+    kWsGather = 8,
+    kWsProbe = 9,
+    kWsCount = 10,
+};
 struct Workspace {
     int device;
     hipStream_t stream;
@@ -164,6 +176,65 @@ int do_build(const vbf::KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, i
     int rc = get_workspace(s, need, &ws);
     if (rc) return rc;
     HIP_TRY(vbf::launch_build_partitioned(kb, m, k, words, ws, need, atomic_merge, s));
+    return VBF_OK;
+}
+
+// The probe every entry point funnels into: out (answer bytes) or count (hits).  The per-key
+// early-exit gather costs ~1 + (k-1)*hit_rate random filter loads per key; the partitioned probe
+// costs all k hashes per key but no random loads.  AUTO (large batches over large filters) probes
+// the first 64K keys with the gather, reads the hit count back (one stream sync) and takes the
+// partitioned path when at least 35 % of them hit (measured crossover: 100M keys, k = 10).
+constexpr uint64_t kAutoProbePartitionMinIdx = 1ull << 24;
+constexpr uint64_t kProbeSample = 1ull << 16;
+
+int do_probe(const vbf::KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+             unsigned long long* count, int strategy, hipStream_t s) {
+    if (kb.n == 0) return VBF_OK;
+    bool part;
+    if (strategy == VBF_BUILD_ATOMIC) {
+        part = false;
+    } else if (strategy == VBF_BUILD_PARTITIONED) {
+        if (!vbf::probe_partition_supported(m, k))
+            return fail(VBF_EINVAL, "partitioned probe needs 1 <= k <= 32 and a filter of at least 1 segment (k = %u)", k);
+        part = true;
+    } else if (strategy == VBF_BUILD_AUTO) {
+        part = k > 1 && vbf::probe_partition_supported(m, k) && kb.n * (uint64_t)k >= kAutoProbePartitionMinIdx &&
+               m >= (64u << 20);
+        if (part) {  // sample the hit rate
+            vbf::KeyBatch sb = kb;
+            sb.n = std::min<uint64_t>(kb.n, kProbeSample);
+            const uint64_t np = vbf::count_partials(sb.n);
+            void* pw = nullptr;
+            int rc = get_workspace(s, np * 4 + 256, &pw, kWsCount);
+            if (rc) return rc;
+            auto* c = reinterpret_cast<unsigned long long*>(static_cast<char*>(pw) + np * 4);
+            c = reinterpret_cast<unsigned long long*>(((uintptr_t)c + 7) & ~(uintptr_t)7);
+            HIP_TRY(hipMemsetAsync(c, 0, 8, s));
+            HIP_TRY(vbf::launch_count(sb, m, k, words, c, static_cast<uint32_t*>(pw), s));
+            unsigned long long hits = 0;
+            HIP_TRY(hipMemcpyAsync(&hits, c, 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            part = hits * 100 >= sb.n * 35;
+        }
+    } else {
+        return fail(VBF_EINVAL, "unknown probe strategy %d", strategy);
+    }
+    if (!part || k == 0) {
+        if (count) {
+            void* pw = nullptr;
+            int rc = get_workspace(s, vbf::count_partials(kb.n) * 4, &pw, kWsCount);
+            if (rc) return rc;
+            HIP_TRY(vbf::launch_count(kb, m, k, words, count, static_cast<uint32_t*>(pw), s));
+        } else {
+            HIP_TRY(vbf::launch_probe(kb, m, k, words, out, s));
+        }
+        return VBF_OK;
+    }
+    const uint64_t need = vbf::probe_workspace_bytes(kb.n, m, k);
+    void* ws = nullptr;
+    int rc = get_workspace(s, need, &ws, kWsProbe);
+    if (rc) return rc;
+    HIP_TRY(vbf::launch_probe_partitioned(kb, m, k, words, out, count, ws, need, s));
     return VBF_OK;
 }
 
@@ -614,28 +685,41 @@ int vbf_build_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stri
     return ok();
 }
 
-int vbf_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
-                  int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
-                  void* stream) {
+int vbf_probe_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                     int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                     int strategy, void* stream) {
     int rc = check_mk(m, k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
     if (n && !out) return fail(VBF_EINVAL, "out is NULL");
     vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
-    HIP_TRY(vbf::launch_probe(kb, m, k, words, out, (hipStream_t)stream));
+    if ((rc = do_probe(kb, m, k, words, out, nullptr, strategy, (hipStream_t)stream))) return rc;
+    return ok();
+}
+
+int vbf_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                  int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                  void* stream) {
+    return vbf_probe_dev_ex(keys, offsets, stride, n, len_prefix, m, k, words, out, VBF_BUILD_AUTO, stream);
+}
+
+int vbf_probe_count_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                           int len_prefix, uint32_t m, uint32_t k, const uint32_t* words,
+                           unsigned long long* count_dev, int strategy, void* stream) {
+    int rc = check_mk(m, k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    if (!count_dev) return fail(VBF_EINVAL, "count_dev is NULL");
+    vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+    if ((rc = do_probe(kb, m, k, words, nullptr, count_dev, strategy, (hipStream_t)stream))) return rc;
     return ok();
 }
 
 int vbf_probe_count_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                         int len_prefix, uint32_t m, uint32_t k, const uint32_t* words,
                         unsigned long long* count_dev, void* stream) {
-    int rc = check_mk(m, k, n);
-    if (rc) return rc;
-    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
-    if (!count_dev) return fail(VBF_EINVAL, "count_dev is NULL");
-    vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
-    HIP_TRY(vbf::launch_count(kb, m, k, words, count_dev, (hipStream_t)stream));
-    return ok();
+    return vbf_probe_count_dev_ex(keys, offsets, stride, n, len_prefix, m, k, words, count_dev, VBF_BUILD_AUTO,
+                                  stream);
 }
 
 int vbf_hashes_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
@@ -733,7 +817,7 @@ int vbf_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
     rc = pipeline_host_keys(
         *st, keys, offsets, stride, n, len_prefix, true,
         [&](const vbf::KeyBatch& kb, uint64_t, int b, hipStream_t s) -> int {
-            HIP_TRY(vbf::launch_probe(kb, m, k, st->d_words, st->d_out[b], s));
+            if (int rc2 = do_probe(kb, m, k, st->d_words, st->d_out[b], nullptr, VBF_BUILD_AUTO, s)) return rc2;
             HIP_TRY(hipMemcpyAsync(st->h_out[b], st->d_out[b], kb.n, hipMemcpyDeviceToHost, s));
             return VBF_OK;
         },
@@ -866,7 +950,7 @@ int vbf_filter_contains_dev(const vbf_filter* f, const uint8_t* keys, const uint
     DEVICE_SCOPE(s.device);
     std::lock_guard<std::mutex> lk(s.mu);
     vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
-    HIP_TRY(vbf::launch_probe(kb, s.m, f->k, s.d_words, out, (hipStream_t)stream));
+    if ((rc = do_probe(kb, s.m, f->k, s.d_words, out, nullptr, VBF_BUILD_AUTO, (hipStream_t)stream))) return rc;
     return ok();
 }
 
@@ -890,7 +974,7 @@ int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uin
     rc = pipeline_host_keys(
         *st, keys, offsets, stride, n, len_prefix, true,
         [&](const vbf::KeyBatch& kb, uint64_t, int b, hipStream_t hs) -> int {
-            HIP_TRY(vbf::launch_probe(kb, s.m, f->k, s.d_words, st->d_out[b], hs));
+            if (int rc2 = do_probe(kb, s.m, f->k, s.d_words, st->d_out[b], nullptr, VBF_BUILD_AUTO, hs)) return rc2;
             HIP_TRY(hipMemcpyAsync(st->h_out[b], st->d_out[b], kb.n, hipMemcpyDeviceToHost, hs));
             return VBF_OK;
         },

@@ -22,7 +22,8 @@ hipError_t launch_build(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* wo
 // Optional per-phase timing (vbf_profile_*): HIP events recorded on the launch stream.
 enum Phase { kPhaseTileSort = 0, kPhaseTranspose = 1, kPhaseSegOr = 2, kPhaseAtomicBuild = 3,
              kPhaseProbe = 4, kPhaseSstWalk = 5, kPhaseSstScan = 6, kPhaseSstEmit = 7,
-             kPhaseMergeLevels = 8, kPhaseFold = 9, kPhaseSelect = 10, kNumPhases = 11 };
+             kPhaseMergeLevels = 8, kPhaseFold = 9, kPhaseSelect = 10, kPhaseProbePack = 11,
+             kPhaseProbeSeg = 12, kPhaseProbeOut = 13, kNumPhases = 14 };
 void phase_begin(int phase, hipStream_t s);
 void phase_end(int phase, hipStream_t s);
 
@@ -31,12 +32,21 @@ void phase_end(int phase, hipStream_t s);
 constexpr uint64_t kPartChunkIdx = 1ull << 30;
 bool partition_supported(uint32_t m, uint32_t k);
 uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
+// Partitioned probe (vbf_partition.hip): out (answer bytes) or count (hits), one of them.
+bool probe_partition_supported(uint32_t m, uint32_t k);
+uint64_t probe_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
+hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                                    unsigned long long* count, void* ws, uint64_t ws_bytes, hipStream_t s);
+uint64_t probe_count_partials(uint64_t n, uint32_t m, uint32_t k);
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
                                     void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s);
 hipError_t launch_probe(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
                         uint8_t* out, hipStream_t s);
+// Count: `partial` holds count_partials(n) u32 of scratch; the hits are added to *count.
+uint64_t count_partials(uint64_t n);
 hipError_t launch_count(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
-                        unsigned long long* count, hipStream_t s);
+                        unsigned long long* count, uint32_t* partial, hipStream_t s);
+hipError_t launch_count_finish(const uint32_t* partial, uint64_t np, unsigned long long* count, hipStream_t s);
 hipError_t launch_hashes(const KeyBatch& kb, uint32_t k, uint64_t* out, hipStream_t s);
 hipError_t launch_or_words(uint32_t* dst, const uint32_t* src, uint64_t nwords, hipStream_t s);
 hipError_t launch_popcount(const uint32_t* words, uint64_t nwords, unsigned long long* out,
