@@ -527,7 +527,7 @@ def main():
     ap.add_argument("--multi", action="store_true", help="batched multi-SST probe (8(f) row 4)")
     ap.add_argument("--strategy", type=int, default=0, help="0 auto, 1 atomic, 2 partitioned")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=2_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--cpu-opt-threads", type=int, default=16)
     args = ap.parse_args()
     ctx = Ctx(args)

@@ -24,7 +24,7 @@ run() {  # run NAME SECONDS CMD...
 for s in $STEPS; do
   case $s in
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) run pytest_gpu 1200 python -m pytest tests -x -q -m gpu ;;
+    pytest) run pytest_gpu 1200 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
     benchq)  run bench_quick 300 python bench.py --no-cpu-baseline ;;
     benchnostagger) run bench_nostagger 300 env VBF_STAGGER=0 python bench.py --no-cpu-baseline ;;
