@@ -5,6 +5,7 @@
 //   gather   : random 32-bit load rate from the same arrays.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 -o tools/ubench tools/ubench.hip
 #include <hip/hip_runtime.h>
+#include <string>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -60,9 +61,22 @@ __device__ __forceinline__ uint64_t add_sw(uint64_t a, uint64_t b) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Rotate by 32 in ONE instruction: v_pk_mov_b32 with op_sel picks the halves crosswise, so the
+// result lands in an aligned pair ready for v_lshl_add_u64 (the plain form costs 2 v_mov_b32).
+__device__ __forceinline__ uint64_t swap_pk(uint64_t x) {
+    uint64_t r;
+    asm("v_pk_mov_b32 %0, %1, %1 op_sel:[1,0]" : "=v"(r) : "v"(x));
+    return r;
+}
+
 template <int V>
 __device__ __forceinline__ void round_(S& s) {
-    if constexpr (V == 0) {
+    if constexpr (V == 6) {
+        s.v0 += s.v1; s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap_pk(s.v0);
+        s.v2 += s.v3; s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
+        s.v0 += s.v3; s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
+        s.v2 += s.v1; s.v1 = rotl_a<17>(s.v1); s.v1 ^= s.v2; s.v2 = swap_pk(s.v2);
+    } else if constexpr (V == 0) {
         s.v0 += s.v1; s.v1 = rotl_c(s.v1, 13); s.v1 ^= s.v0; s.v0 = rotl_c(s.v0, 32);
         s.v2 += s.v3; s.v3 = rotl_c(s.v3, 16); s.v3 ^= s.v2;
         s.v0 += s.v3; s.v3 = rotl_c(s.v3, 21); s.v3 ^= s.v0;
@@ -139,12 +153,12 @@ __global__ __launch_bounds__(BS) void k_hash2(uint64_t n, int k, uint64_t m, uin
     extern __shared__ uint32_t pad[];
     uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
     if (j >= n) return;
-    constexpr int V = MODE == 3 ? 3 : MODE == 5 ? 5 : 1;
+    constexpr int V = MODE == 3 ? 3 : MODE == 5 ? 5 : MODE == 6 ? 6 : MODE == 7 ? 6 : 1;
     S s{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL, 0x7465646279746573ULL};
     if constexpr (V == 5) s.v2 = swap32(s.v2);  // stored form
     comp<V>(s, 16); comp<V>(s, j * 0x9E3779B97F4A7C15ULL); comp<V>(s, j);
     uint64_t acc = 0;
-    if constexpr (MODE == 2) {
+    if constexpr (MODE == 2 || MODE == 7) {
         int i = 0;
         for (; i + 1 < k; i += 2) {
             S t0 = s, t1 = s;
@@ -261,11 +275,23 @@ __global__ void k_hash_check(uint64_t* out) {
     out[j] = fin<V>(s, 32ull << 56);
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool hash_only = argc > 1 && std::string(argv[1]) == "hash";
     const uint64_t n = 100000000;
     uint64_t* out;
     CHECK(hipMalloc(&out, 8));
     const unsigned blocks = (unsigned)((n + 255) / 256);
+    {
+        uint64_t *c1, *c6;
+        CHECK(hipMalloc(&c1, 64 * 8)); CHECK(hipMalloc(&c6, 64 * 8));
+        hipLaunchKernelGGL(k_hash_check<1>, dim3(1), dim3(64), 0, 0, c1);
+        hipLaunchKernelGGL(k_hash_check<6>, dim3(1), dim3(64), 0, 0, c6);
+        uint64_t h1[64], h6[64];
+        CHECK(hipMemcpy(h1, c1, 512, hipMemcpyDeviceToHost)); CHECK(hipMemcpy(h6, c6, 512, hipMemcpyDeviceToHost));
+        int bad = 0;
+        for (int i = 0; i < 64; ++i) bad += h1[i] != h6[i];
+        printf("V6 (v_pk_mov_b32 swap) == V1 hashes: %s\n", bad ? "MISMATCH" : "ok");
+    }
     {
         uint64_t *c1, *c5;
         CHECK(hipMalloc(&c1, 64 * 8)); CHECK(hipMalloc(&c5, 64 * 8));
@@ -296,10 +322,15 @@ int main() {
         run(k_hash2<2, 256>, 256, 0, "V1 2-seed interleave + mod, 256 thr");
         run(k_hash2<3, 256>, 256, 0, "V3 addc + mod, 256 thr");
         run(k_hash2<5, 256>, 256, 0, "V5 swap-folded carry adds + mod, 256 thr");
+        run(k_hash2<6, 256>, 256, 0, "V6 pk_mov swap + mod, 256 thr");
+        run(k_hash2<7, 256>, 256, 0, "V6 pk_mov swap, 2-seed + mod, 256 thr");
+        run(k_hash2<6, 1024>, 1024, 80 * 1024, "V6 pk_mov swap + mod, 1024 thr, 2 blocks/CU");
+        run(k_hash2<1, 1024>, 1024, 80 * 1024, "V1 + mod, 1024 thr, 2 blocks/CU");
         run(k_hash2<1, 1024>, 1024, 120 * 1024, "V1 + mod, 1024 thr, 1 block/CU (LDS)");
         run(k_hash2<2, 1024>, 1024, 120 * 1024, "V1 2-seed + mod, 1024 thr, 1 block/CU");
         run(k_hash2<3, 1024>, 1024, 120 * 1024, "V3 addc + mod, 1024 thr, 1 block/CU");
     }
+    if (hash_only) return 0;
     {
         uint32_t* o;
         CHECK(hipMalloc(&o, 4));

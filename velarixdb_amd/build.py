@@ -27,10 +27,24 @@ def needs_build():
 
 
 def build(force=False, verbose=False):
+    """One hipcc per translation unit, in parallel, then one link."""
     if not force and not needs_build():
         return OUT
-    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++20", "-fPIC", "-shared", "-Wall",
-           "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    objdir = os.path.join(HERE, "..", "build", "obj")
+    os.makedirs(objdir, exist_ok=True)
+    flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++20", "-fPIC", "-Wall"]
+    procs, objs = [], []
+    for s in SOURCES:
+        obj = os.path.join(objdir, s.replace(".hip", ".o"))
+        objs.append(obj)
+        cmd = [_hipcc()] + flags + ["-c", os.path.join(CSRC, s), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((s, subprocess.Popen(cmd, cwd=CSRC)))
+    failed = [s for s, p in procs if p.wait() != 0]
+    if failed:
+        raise RuntimeError("hipcc failed for " + ", ".join(failed))
+    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd, cwd=CSRC)

@@ -61,6 +61,7 @@ struct PartPlan {
     uint32_t lds1;        // K1 dynamic LDS bytes
     uint32_t stagger_lo, stagger_hi, stagger_sleeps;
     uint32_t ablate;      // timing experiments only (VBF_ABLATE): 1 skip place+copy, 2 also count
+    uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or)
     uint64_t m, mu, nwords;
 };
 
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = fast_mod(prefix_hash(p, i), pl.m, pl.mu);
-                    if (pl.ablate != 2) atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    atomicAdd(&cnt[idx >> kSegBits], 1u);
                 }
                 stash[r * K + i] = idx;
             }
@@ -264,7 +265,16 @@ __device__ __forceinline__ void load8(const uint32_t* tile, uint32_t cp, uint32_
     nib = (uint32_t)(hh >> ((e & 7) * 4));
 }
 
-__global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const uint16_t* endsT,
+// K3 tile-loop variants (VBF_K3, speed only; identical results):
+//   0: two-stage -- run bounds of batch b+1 (8 u16 loads per lane) in flight with batch b's data
+//   2: two-stage, bounds loaded coalesced (one u16 per lane for the wave's 64 tiles) and handed
+//      to the 8-lane groups with ds_bpermute
+//   3: three-stage -- bounds of b+2, data of b+1 and the ORs of b overlap; data loads are
+//      unconditional (idle lanes re-read their run's first 8 entries) so vmcnt waits stay exact;
+//      NG runs per 8-lane group per batch (3: 1024 threads NG=4; 4: 1024, NG=5; 5: 768, NG=6;
+//      6: 768, NG=8)
+template <int V, int BS = kPBlock, int NG = 8>
+__global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint16_t* endsT,
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
                                                     uint32_t* words) {
     __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
@@ -278,7 +288,7 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     const uint64_t wbase = (uint64_t)seg * kSegWords;
     const uint32_t wn = (uint32_t)std::min<uint64_t>(kSegWords, pl.nwords - wbase);
     const bool own = (pl.G == 1) && !atomic_merge;  // sole writer: start from the existing words
-    for (uint32_t w = tid * 4; w < kSegWords; w += kPBlock * 4) {
+    for (uint32_t w = tid * 4; w < kSegWords; w += BS * 4) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (own && pl.ablate < 6) {
             if (w + 4 <= wn)
@@ -293,82 +303,177 @@ __global__ __launch_bounds__(kPBlock) void k_seg_or(const uint32_t* tiles, const
     }
     __syncthreads();
 
-    if (pl.ablate < 5) {  // 5-7: timing experiments, fixed costs only
     const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / pl.G);
     const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / pl.G);
     const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
     const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * ntiles : nullptr;
     const uint32_t grp = lane >> 3, q8 = (lane & 7) * 8;
-    // Two-stage pipeline over the wave's 64-tile batches: the run bounds of batch b+1 and the
-    // data of batch b are in flight together, so each batch costs one memory latency, not two.
-    auto bounds = [&](uint32_t tg, uint32_t (&st)[8], uint32_t (&len)[8]) {
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const uint32_t t = tg + g * 8 + grp;  // the 8 lanes of a group read the same u16
-            uint32_t b = 0, e = 0;
-            if (t < t_hi) {
-                b = row_beg ? row_beg[t] : 0;
-                e = row_end[t];
-            }
-            st[g] = b;
-            len[g] = e - b;
+    // a wave serves 8 * NG tiles per batch (8-lane groups, NG runs each)
+    const uint32_t step = (BS / 64) * 8 * NG;
+    uint32_t tg = t_lo + wave * 8 * NG;
+    // runs longer than 64 indices (rare at the default plan; common for tiny m)
+    auto tail = [&](uint32_t t, uint32_t st, uint32_t len) {
+        const uint32_t* tile = tiles + (uint64_t)t * pl.tile_words;
+#pragma unroll 1
+        for (uint32_t e = q8 + 64; e < len; e += 64) {
+            uint4 lt;
+            uint32_t nt;
+            load8(tile, pl.CP, st + e, lt, nt);
+            or8(bitmap, lt, nt, std::min<uint32_t>(8, len - e));
         }
     };
-    const uint32_t step = kPBlock;  // 16 waves x 64 tiles
-    uint32_t tg = t_lo + wave * 64;
-    uint32_t st[8], len[8];
-    bounds(tg, st, len);
-    while (tg < t_hi) {
-        uint32_t nib[8];
-        uint4 l[8];
+    // packed bounds (begin | end << 16) of tile tg + lane, one coalesced u16 pair per lane
+    auto lb = [&](uint32_t t0) -> uint32_t {
+        const uint32_t t = t0 + lane;
+        uint32_t v = 0;
+        if (t < t_hi) v = (row_beg ? (uint32_t)row_beg[t] : 0u) | ((uint32_t)row_end[t] << 16);
+        return v;
+    };
+
+    if (pl.ablate >= 5) {
+        // 5-7: timing experiments, fixed costs only
+    } else if constexpr (V == 3) {
+        struct Batch {
+            uint32_t be[NG];
+            uint4 l[NG];
+            uint32_t nib[NG];
+        };
+        auto spread = [&](uint32_t v, Batch& b) {
 #pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            if (q8 < len[g]) {
-                const uint32_t* tile = tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words;
-                if (pl.ablate == 4) {  // timing experiment: synthetic indices, no tile loads
-                    l[g] = make_uint4(tg * 2654435761u + g, lane * 40503u, tg ^ lane, g * 977u);
-                    nib[g] = tg + lane;
-                } else {
-                    load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
+            for (int g = 0; g < NG; ++g) b.be[g] = (uint32_t)__shfl((int)v, g * 8 + grp);
+        };
+        auto issue = [&](uint32_t t0, Batch& b) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const uint32_t st = b.be[g] & 0xFFFFu, len = (b.be[g] >> 16) - st;
+                const uint32_t t = std::min(t0 + g * 8 + grp, t_hi - 1);
+                // idle lanes re-read the run's first 8 entries (same lines, always in bounds)
+                const uint32_t e = q8 < len ? st + q8 : st;
+                load8(tiles + (uint64_t)t * pl.tile_words, pl.CP, e, b.l[g], b.nib[g]);
+            }
+        };
+        auto consume = [&](uint32_t t0, const Batch& b) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const uint32_t st = b.be[g] & 0xFFFFu, len = (b.be[g] >> 16) - st;
+                if (q8 < len) or8(bitmap, b.l[g], b.nib[g], std::min<uint32_t>(8, len - q8));
+            }
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const uint32_t st = b.be[g] & 0xFFFFu, len = (b.be[g] >> 16) - st;
+                if (len > 64) tail(t0 + g * 8 + grp, st, len);
+            }
+        };
+        Batch A, B;
+        uint32_t v0 = lb(tg), v1 = lb(tg + step);
+        spread(v0, A);
+        if (tg < t_hi) issue(tg, A);
+        // invariant at the top: A = batch tg (data in flight), v1 = bounds of tg + step
+        while (tg < t_hi) {
+            spread(v1, B);
+            uint32_t v2 = lb(tg + 2 * step);
+            const bool more = tg + step < t_hi;
+            if (more) issue(tg + step, B);
+            consume(tg, A);
+            tg += step;
+            if (!more) break;
+            v1 = v2;
+            spread(v1, A);
+            v2 = lb(tg + 2 * step);
+            const bool more2 = tg + step < t_hi;
+            if (more2) issue(tg + step, A);
+            consume(tg, B);
+            tg += step;
+            if (!more2) break;
+            v1 = v2;
+        }
+    } else if constexpr (V == 2) {
+        uint32_t v = lb(tg);
+        while (tg < t_hi) {
+            uint32_t be[8];
+            uint4 l[8];
+            uint32_t nib[8];
+#pragma unroll
+            for (int g = 0; g < 8; ++g) be[g] = (uint32_t)__shfl((int)v, g * 8 + grp);
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t st = be[g] & 0xFFFFu, len = (be[g] >> 16) - st;
+                if (q8 < len) load8(tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words, pl.CP, st + q8, l[g], nib[g]);
+            }
+            v = lb(tg + step);
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t st = be[g] & 0xFFFFu, len = (be[g] >> 16) - st;
+                if (q8 < len) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len - q8));
+            }
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t st = be[g] & 0xFFFFu, len = (be[g] >> 16) - st;
+                if (len > 64) tail(tg + g * 8 + grp, st, len);
+            }
+            tg += step;
+        }
+    } else {
+        // Two-stage pipeline over the wave's 64-tile batches: the run bounds of batch b+1 and the
+        // data of batch b are in flight together, so each batch costs one memory latency, not two.
+        auto bounds = [&](uint32_t t0, uint32_t (&st)[8], uint32_t (&len)[8]) {
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                const uint32_t t = t0 + g * 8 + grp;  // the 8 lanes of a group read the same u16
+                uint32_t b = 0, e = 0;
+                if (t < t_hi) {
+                    b = row_beg ? row_beg[t] : 0;
+                    e = row_end[t];
+                }
+                st[g] = b;
+                len[g] = e - b;
+            }
+        };
+        uint32_t st[8], len[8];
+        bounds(tg, st, len);
+        while (tg < t_hi) {
+            uint32_t nib[8];
+            uint4 l[8];
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                if (q8 < len[g]) {
+                    const uint32_t* tile = tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words;
+                    if (pl.ablate == 4) {  // timing experiment: synthetic indices, no tile loads
+                        l[g] = make_uint4(tg * 2654435761u + g, lane * 40503u, tg ^ lane, g * 977u);
+                        nib[g] = tg + lane;
+                    } else {
+                        load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
+                    }
                 }
             }
-        }
-        const uint32_t tn = tg + step;
-        uint32_t st2[8], len2[8];
-        bounds(tn, st2, len2);
+            const uint32_t tn = tg + step;
+            uint32_t st2[8], len2[8];
+            bounds(tn, st2, len2);
 #pragma unroll
-        for (int g = 0; g < 8; ++g)
-            if (q8 < len[g]) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len[g] - q8), pl.ablate);
-        // tail: runs longer than 64 indices (rare at the default plan; common for tiny m)
-#pragma unroll 1
-        for (int g = 0; g < 8; ++g) {
-            const uint32_t* tile = tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words;
-            for (uint32_t e = q8 + 64; e < len[g]; e += 64) {
-                uint4 lt;
-                uint32_t nt;
-                load8(tile, pl.CP, st[g] + e, lt, nt);
-                or8(bitmap, lt, nt, std::min<uint32_t>(8, len[g] - e));
+            for (int g = 0; g < 8; ++g)
+                if (q8 < len[g]) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len[g] - q8), pl.ablate);
+#pragma unroll
+            for (int g = 0; g < 8; ++g)
+                if (len[g] > 64) tail(tg + g * 8 + grp, st[g], len[g]);
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+                st[g] = st2[g];
+                len[g] = len2[g];
             }
+            tg = tn;
         }
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            st[g] = st2[g];
-            len[g] = len2[g];
-        }
-        tg = tn;
-    }
     }
     __syncthreads();
     if (pl.ablate == 7) return;
     if (own) {
-        for (uint32_t w = tid * 4; w < wn; w += kPBlock * 4) {
+        for (uint32_t w = tid * 4; w < wn; w += BS * 4) {
             if (w + 4 <= wn)
                 *reinterpret_cast<uint4*>(words + wbase + w) = *reinterpret_cast<const uint4*>(bitmap + w);
             else
                 for (uint32_t x = w; x < wn; ++x) words[wbase + x] = bitmap[x];
         }
     } else {
-        for (uint32_t w = tid; w < wn; w += kPBlock) {
+        for (uint32_t w = tid; w < wn; w += BS) {
             const uint32_t v = bitmap[w];
             if (v) atomicOr(words + wbase + w, v);
         }
@@ -411,6 +516,8 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.stagger_sleeps = sleeps;
     static const int abl = [] { const char* e = getenv("VBF_ABLATE"); return e ? atoi(e) : 0; }();
     pl.ablate = (uint32_t)abl;
+    static const int k3v = [] { const char* e = getenv("VBF_K3"); return e ? atoi(e) : 4; }();
+    pl.k3v = (uint32_t)k3v;
     return pl;
 }
 
@@ -476,8 +583,14 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         const bool merge = atomic_merge || pl.G > 1;
         phase_end(kPhaseTranspose, s);
         phase_begin(kPhaseSegOr, s);
-        hipLaunchKernelGGL(k_seg_or, dim3(pl.nseg * pl.G), dim3(kPBlock), 0, s, tiles, endsT, ntiles, pl,
-                           merge, words);
+        auto k3 = pl.k3v == 3 ? k_seg_or<3, kPBlock, 4>
+                : pl.k3v == 4 ? k_seg_or<3, kPBlock, 5>
+                : pl.k3v == 5 ? k_seg_or<3, 768, 6>
+                : pl.k3v == 6 ? k_seg_or<3, 768, 8>
+                : pl.k3v == 2 ? k_seg_or<2>
+                              : k_seg_or<0>;
+        const int bs = (pl.k3v == 5 || pl.k3v == 6) ? 768 : kPBlock;
+        hipLaunchKernelGGL(k3, dim3(pl.nseg * pl.G), dim3(bs), 0, s, tiles, endsT, ntiles, pl, merge, words);
         phase_end(kPhaseSegOr, s);
         err = hipGetLastError();
         if (err != hipSuccess) return err;
