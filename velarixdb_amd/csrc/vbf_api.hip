@@ -16,6 +16,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/vbf.h"
@@ -244,6 +245,32 @@ int do_probe(const vbf::KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* wo
 // ---------------------------------------------------------------------------------------
 constexpr uint64_t kChunkBytes = 64ull << 20;
 
+// Host copy into / out of the pinned staging buffers, split over up to 8 threads
+// (VBF_COPY_THREADS): one thread's memcpy into pinned memory runs well below the PCIe rate.
+void par_memcpy(void* dst, const void* src, size_t n) {
+    constexpr size_t kMinPerThread = 4u << 20;
+    static const unsigned nt_max = [] {
+        const char* e = getenv("VBF_COPY_THREADS");
+        const unsigned hw = std::thread::hardware_concurrency();
+        const int v = e ? atoi(e) : (int)std::min(8u, hw ? hw : 1u);
+        return (unsigned)std::max(1, v);
+    }();
+    const unsigned nt = (unsigned)std::min<size_t>(nt_max, n / kMinPerThread);
+    if (nt <= 1) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = (n / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (unsigned t = 1; t < nt && t * per < n; ++t) {
+        const size_t a = t * per, len = std::min(per, n - a);
+        th.emplace_back([=] { std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, len); });
+    }
+    std::memcpy(dst, src, std::min(per, n));
+    for (auto& x : th) x.join();
+}
+
 struct Staging {
     std::mutex mu;
     int device = -1;
@@ -260,6 +287,7 @@ struct Staging {
     uint64_t out_cap[2] = {0, 0};
     uint32_t* d_words = nullptr;  // scratch filter for the one-shot host API
     uint64_t words_cap = 0;
+    uint8_t* h_xfer[2] = {nullptr, nullptr};  // pinned bounce buffers for large filter copies
 
     int init(int dev) {
         if (device == dev) return VBF_OK;
@@ -285,6 +313,70 @@ struct Staging {
         return VBF_OK;
     }
 };
+
+// Large host <-> device copies (filter words) bounce through two pinned chunk buffers, so the
+// DMA of chunk c+1 overlaps the (threaded) host copy of chunk c; pageable hipMemcpy runs at a
+// fraction of the link rate.  Small copies go direct.  Caller holds st.mu and has ordered src.
+constexpr uint64_t kXferDirect = 8ull << 20;
+
+int xfer_bufs(Staging& st) {
+    for (int b = 0; b < 2; ++b)
+        if (!st.h_xfer[b]) HIP_TRY(hipHostMalloc((void**)&st.h_xfer[b], kChunkBytes, hipHostMallocDefault));
+    return VBF_OK;
+}
+
+int xfer_d2h(Staging& st, void* dst, const void* src, uint64_t bytes) {
+    if (bytes < kXferDirect) {
+        HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+        return VBF_OK;
+    }
+    int rc = xfer_bufs(st);
+    if (rc) return rc;
+    const uint64_t nc = (bytes + kChunkBytes - 1) / kChunkBytes;
+    for (uint64_t c = 0; c <= nc; ++c) {
+        if (c < nc) {
+            const int b = (int)(c & 1);
+            const uint64_t off = c * kChunkBytes, len = std::min<uint64_t>(kChunkBytes, bytes - off);
+            HIP_TRY(hipMemcpyAsync(st.h_xfer[b], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost,
+                                   st.stream[b]));
+            HIP_TRY(hipEventRecord(st.done[b], st.stream[b]));
+        }
+        if (c > 0) {
+            const int pb = (int)((c - 1) & 1);
+            const uint64_t off = (c - 1) * kChunkBytes, len = std::min<uint64_t>(kChunkBytes, bytes - off);
+            HIP_TRY(hipEventSynchronize(st.done[pb]));
+            par_memcpy(static_cast<char*>(dst) + off, st.h_xfer[pb], len);
+        }
+    }
+    return VBF_OK;
+}
+
+// H2D on st.stream[0..1]; returns with both streams synchronized.
+int xfer_h2d(Staging& st, void* dst, const void* src, uint64_t bytes) {
+    if (bytes < kXferDirect) {
+        HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+        return VBF_OK;
+    }
+    int rc = xfer_bufs(st);
+    if (rc) return rc;
+    const uint64_t nc = (bytes + kChunkBytes - 1) / kChunkBytes;
+    for (uint64_t c = 0; c < nc; ++c) {
+        const int b = (int)(c & 1);
+        const uint64_t off = c * kChunkBytes, len = std::min<uint64_t>(kChunkBytes, bytes - off);
+        if (c >= 2) HIP_TRY(hipEventSynchronize(st.done[b]));  // buffer b's previous DMA finished
+        par_memcpy(st.h_xfer[b], static_cast<const char*>(src) + off, len);
+        HIP_TRY(hipMemcpyAsync(static_cast<char*>(dst) + off, st.h_xfer[b], len, hipMemcpyHostToDevice, st.stream[b]));
+        HIP_TRY(hipEventRecord(st.done[b], st.stream[b]));
+    }
+    for (int b = 0; b < 2; ++b) HIP_TRY(hipStreamSynchronize(st.stream[b]));
+    return VBF_OK;
+}
+
+// VBF_H2D_DIRECT=0 forces the pinned bounce for key chunks (A/B); default: direct.
+bool h2d_direct() {
+    static const bool v = [] { const char* e = getenv("VBF_H2D_DIRECT"); return !e || atoi(e) != 0; }();
+    return v;
+}
 
 std::mutex g_staging_mu;
 std::vector<std::unique_ptr<Staging>> g_staging;
@@ -328,15 +420,24 @@ int pipeline_host_keys(Staging& st, const uint8_t* keys, const uint64_t* offsets
             if (rc) return rc;
             pending[b] = false;
         }
-        int rc = Staging::grow(&st.h_keys[b], &st.d_keys[b], &st.key_cap[b], bytes ? bytes : 1);
-        if (rc) return rc;
-        if (bytes) std::memcpy(st.h_keys[b], keys + (offsets ? base : lo * stride), bytes);
-        HIP_TRY(hipMemcpyAsync(st.d_keys[b], st.h_keys[b], bytes, hipMemcpyHostToDevice, st.stream[b]));
+        const uint8_t* src = keys + (offsets ? base : lo * stride);
+        int rc;
+        if (h2d_direct()) {
+            // the runtime's own pageable path runs at the link rate: no host bounce copy
+            rc = Staging::grow<uint8_t>(nullptr, &st.d_keys[b], &st.key_cap[b], bytes ? bytes : 1);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpyAsync(st.d_keys[b], src, bytes, hipMemcpyHostToDevice, st.stream[b]));
+        } else {
+            rc = Staging::grow(&st.h_keys[b], &st.d_keys[b], &st.key_cap[b], bytes ? bytes : 1);
+            if (rc) return rc;
+            if (bytes) par_memcpy(st.h_keys[b], src, bytes);
+            HIP_TRY(hipMemcpyAsync(st.d_keys[b], st.h_keys[b], bytes, hipMemcpyHostToDevice, st.stream[b]));
+        }
         const uint64_t* d_off = nullptr;
         if (offsets) {
             rc = Staging::grow(&st.h_offs[b], &st.d_offs[b], &st.off_cap[b], hi - lo + 1);
             if (rc) return rc;
-            std::memcpy(st.h_offs[b], offsets + lo, (hi - lo + 1) * sizeof(uint64_t));
+            par_memcpy(st.h_offs[b], offsets + lo, (hi - lo + 1) * sizeof(uint64_t));
             HIP_TRY(hipMemcpyAsync(st.d_offs[b], st.h_offs[b], (hi - lo + 1) * sizeof(uint64_t),
                                    hipMemcpyHostToDevice, st.stream[b]));
             d_off = st.d_offs[b];
@@ -782,9 +883,7 @@ int vbf_build_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
     std::lock_guard<std::mutex> lk(st->mu);
     if ((rc = st->init(device))) return rc;
     if ((rc = Staging::grow<uint32_t>(nullptr, &st->d_words, &st->words_cap, need))) return rc;
-    HIP_TRY(hipMemcpyAsync(st->d_words, words, need * 4, hipMemcpyHostToDevice, st->stream[0]));
-    HIP_TRY(hipEventRecord(st->done[0], st->stream[0]));
-    HIP_TRY(hipStreamWaitEvent(st->stream[1], st->done[0], 0));
+    if ((rc = xfer_h2d(*st, st->d_words, words, need * 4))) return rc;
     rc = pipeline_host_keys(
         *st, keys, offsets, stride, n, len_prefix, false,
         [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t s) -> int {
@@ -792,7 +891,7 @@ int vbf_build_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
         },
         [](int, uint64_t, uint64_t) { return VBF_OK; });
     if (rc) return rc;
-    HIP_TRY(hipMemcpy(words, st->d_words, need * 4, hipMemcpyDeviceToHost));
+    if ((rc = xfer_d2h(*st, words, st->d_words, need * 4))) return rc;
     return ok();
 }
 
@@ -822,7 +921,7 @@ int vbf_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
             return VBF_OK;
         },
         [&](int b, uint64_t lo, uint64_t cnt) {
-            std::memcpy(out + lo, st->h_out[b], cnt);
+            par_memcpy(out + lo, st->h_out[b], cnt);
             return VBF_OK;
         });
     if (rc) return rc;
@@ -979,7 +1078,7 @@ int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uin
             return VBF_OK;
         },
         [&](int b, uint64_t lo, uint64_t cnt) {
-            std::memcpy(out + lo, st->h_out[b], cnt);
+            par_memcpy(out + lo, st->h_out[b], cnt);
             return VBF_OK;
         });
     if (rc) return rc;
@@ -1010,8 +1109,11 @@ int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords
     DEVICE_SCOPE(s.device);
     std::lock_guard<std::mutex> lk(s.mu);
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(out, s.d_words, s.nwords * 4, hipMemcpyDeviceToHost));
-    return ok();
+    Staging* st = staging_for(s.device);
+    std::lock_guard<std::mutex> lk2(st->mu);
+    int rc = st->init(s.device);
+    if (!rc) rc = xfer_d2h(*st, out, s.d_words, s.nwords * 4);
+    return rc ? rc : ok();
 }
 
 int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nwords) {
@@ -1023,8 +1125,11 @@ int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nword
     DEVICE_SCOPE(s.device);
     std::lock_guard<std::mutex> lk(s.mu);
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(s.d_words, in, s.nwords * 4, hipMemcpyHostToDevice));
-    return ok();
+    Staging* st = staging_for(s.device);
+    std::lock_guard<std::mutex> lk2(st->mu);
+    int rc = st->init(s.device);
+    if (!rc) rc = xfer_h2d(*st, s.d_words, in, s.nwords * 4);
+    return rc ? rc : ok();
 }
 
 // ---- SST data.db decode ----
