@@ -705,6 +705,12 @@ __global__ __launch_bounds__(kPBlock) void k_probe_pack(DevKeys dk, ProbePlan pl
     }
 }
 
+// Q3 variants (VBF_Q3, speed only; identical answers):
+//   0: one pass per 8-lane group and tile, 8 tiles per wave-step
+//   1: the k_seg_or<3> scheme -- a wave serves 8 * NG tiles per batch, run bounds loaded
+//      coalesced and spread with ds_bpermute, bounds of b+2 / entries of b+1 / bit tests of b in
+//      flight together, unconditional entry loads (idle lanes re-read their run's start)
+template <int V, int NG = 4>
 __global__ __launch_bounds__(kPBlock) void k_probe_seg(const uint32_t* tiles, const uint16_t* endsT, uint32_t ntiles,
                                                        ProbePlan pl, uint32_t G, const uint32_t* words, uint8_t* res) {
     __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
@@ -730,21 +736,96 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg(const uint32_t* tiles, co
     const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
     const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * ntiles : nullptr;
     const uint32_t grp = lane >> 3, q8 = (lane & 7) * 8;
-    // 8-lane group per tile, 8 tiles per wave-step: each lane tests 8 entries -> 1 byte
-    for (uint32_t t = t_lo + wave * 8 + grp; t < t_hi; t += (kPBlock / 64) * 8) {
-        const uint32_t beg = row_beg ? row_beg[t] : 0, end = row_end[t];
-        const uint32_t* run = tiles + (uint64_t)t * pl.cap;
-        for (uint32_t x = beg + q8; x < end; x += 64) {
-            const uint4 a = *reinterpret_cast<const uint4*>(run + x);
-            const uint4 b = *reinterpret_cast<const uint4*>(run + x + 4);
-            const uint32_t e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-            uint32_t r = 0;
+    // 8 entries -> 1 result byte (bit c = entry c's filter bit)
+    auto test8 = [&](const uint4& a, const uint4& b) -> uint32_t {
+        const uint32_t e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t r = 0;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const uint32_t off = e[c] & kOffMask;
-                r |= ((bitmap[off >> 5] >> (off & 31)) & 1u) << c;
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t off = e[c] & kOffMask;
+            r |= ((bitmap[off >> 5] >> (off & 31)) & 1u) << c;
+        }
+        return r;
+    };
+    if constexpr (V == 1) {
+        const uint32_t step = (kPBlock / 64) * 8 * NG;
+        uint32_t tg = t_lo + wave * 8 * NG;
+        auto lb = [&](uint32_t t0) -> uint32_t {
+            const uint32_t t = t0 + lane;
+            uint32_t v = 0;
+            if (t < t_hi) v = (row_beg ? (uint32_t)row_beg[t] : 0u) | ((uint32_t)row_end[t] << 16);
+            return v;
+        };
+        struct Batch {
+            uint32_t be[NG];
+            uint4 a[NG], b[NG];
+        };
+        auto spread = [&](uint32_t v, Batch& bt) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) bt.be[g] = (uint32_t)__shfl((int)v, g * 8 + grp);
+        };
+        auto issue = [&](uint32_t t0, Batch& bt) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const uint32_t st = bt.be[g] & 0xFFFFu, len = (bt.be[g] >> 16) - st;
+                const uint32_t t = std::min(t0 + g * 8 + grp, t_hi - 1);
+                const uint32_t x = q8 < len ? st + q8 : st;
+                const uint32_t* run = tiles + (uint64_t)t * pl.cap + x;
+                bt.a[g] = *reinterpret_cast<const uint4*>(run);
+                bt.b[g] = *reinterpret_cast<const uint4*>(run + 4);
             }
-            res[((uint64_t)t * pl.cap + x) >> 3] = (uint8_t)r;
+        };
+        auto consume = [&](uint32_t t0, const Batch& bt) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const uint32_t st = bt.be[g] & 0xFFFFu, len = (bt.be[g] >> 16) - st;
+                const uint64_t t = t0 + g * 8 + grp;
+                if (q8 < len) res[(t * pl.cap + st + q8) >> 3] = (uint8_t)test8(bt.a[g], bt.b[g]);
+            }
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {  // runs longer than 64 entries
+                const uint32_t st = bt.be[g] & 0xFFFFu, len = (bt.be[g] >> 16) - st;
+                const uint64_t t = t0 + g * 8 + grp;
+#pragma unroll 1
+                for (uint32_t x = st + q8 + 64; x < st + len; x += 64) {
+                    const uint32_t* run = tiles + t * pl.cap + x;
+                    res[(t * pl.cap + x) >> 3] =
+                        (uint8_t)test8(*reinterpret_cast<const uint4*>(run), *reinterpret_cast<const uint4*>(run + 4));
+                }
+            }
+        };
+        Batch A, B;
+        uint32_t v0 = lb(tg), v1 = lb(tg + step);
+        spread(v0, A);
+        if (tg < t_hi) issue(tg, A);
+        while (tg < t_hi) {
+            spread(v1, B);
+            uint32_t v2 = lb(tg + 2 * step);
+            const bool more = tg + step < t_hi;
+            if (more) issue(tg + step, B);
+            consume(tg, A);
+            tg += step;
+            if (!more) break;
+            v1 = v2;
+            spread(v1, A);
+            v2 = lb(tg + 2 * step);
+            const bool more2 = tg + step < t_hi;
+            if (more2) issue(tg + step, A);
+            consume(tg, B);
+            tg += step;
+            if (!more2) break;
+            v1 = v2;
+        }
+    } else {
+        // 8-lane group per tile, 8 tiles per wave-step: each lane tests 8 entries -> 1 byte
+        for (uint32_t t = t_lo + wave * 8 + grp; t < t_hi; t += (kPBlock / 64) * 8) {
+            const uint32_t beg = row_beg ? row_beg[t] : 0, end = row_end[t];
+            const uint32_t* run = tiles + (uint64_t)t * pl.cap;
+            for (uint32_t x = beg + q8; x < end; x += 64) {
+                const uint4 a = *reinterpret_cast<const uint4*>(run + x);
+                const uint4 b = *reinterpret_cast<const uint4*>(run + x + 4);
+                res[((uint64_t)t * pl.cap + x) >> 3] = (uint8_t)test8(a, b);
+            }
         }
     }
 }
@@ -762,10 +843,17 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out(const uint32_t* tiles, co
     __syncthreads();
     const uint32_t total = ends[(uint64_t)blockIdx.x * pl.nseg + pl.nseg - 1];
     const uint32_t* tl = tiles + (uint64_t)blockIdx.x * pl.cap;
-    const uint8_t* rs = res + ((uint64_t)blockIdx.x * pl.cap >> 3);
-    for (uint32_t x = tid; x < total; x += kPBlock) {
-        if (!((rs[x >> 3] >> (x & 7)) & 1u)) {
-            const uint32_t local = tl[x] >> kSegBits;
+    // 32 result bits per lane (cap is a multiple of 32, so each tile's bytes are dword aligned);
+    // only the clear bits -- entries whose filter bit is 0 -- cost a tile read and an LDS AND
+    const uint32_t* rs = reinterpret_cast<const uint32_t*>(res + ((uint64_t)blockIdx.x * pl.cap >> 3));
+    for (uint32_t w = tid; w * 32 < total; w += kPBlock) {
+        const uint32_t valid = std::min<uint32_t>(32, total - w * 32);
+        uint32_t z = ~rs[w];
+        if (valid < 32) z &= (1u << valid) - 1u;
+        while (z) {
+            const uint32_t c = __builtin_ctz(z);
+            z &= z - 1;
+            const uint32_t local = tl[w * 32 + c] >> kSegBits;
             atomicAnd(&ok[local >> 5], ~(1u << (local & 31)));
         }
     }
@@ -803,7 +891,7 @@ static ProbePlan make_probe_plan(uint32_t m, uint32_t k) {
     pl.KT = (uint32_t)std::max<int64_t>(kt, 1);
     pl.R = (pl.KT + kPBlock - 1) / kPBlock;
     pl.C = pl.KT * k;
-    pl.cap = (pl.C + 7 * pl.nseg + 7) & ~7u;
+    pl.cap = (pl.C + 7 * pl.nseg + 31) & ~31u;  // multiple of 32: k_probe_out reads result dwords
     pl.lds1 = (pl.C + 2 * pl.nseg_pad + 16) * 4;
     return pl;
 }
@@ -875,7 +963,9 @@ hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         phase_end(kPhaseProbePack, s);
         phase_begin(kPhaseProbeSeg, s);
         const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
-        hipLaunchKernelGGL(k_probe_seg, dim3(pl.nseg * G), dim3(kPBlock), 0, s, tiles, endsT, ntiles, pl, G, words,
+        static const int q3v = [] { const char* e = getenv("VBF_Q3"); return e ? atoi(e) : 1; }();
+        hipLaunchKernelGGL(q3v == 1 ? k_probe_seg<1> : k_probe_seg<0>, dim3(pl.nseg * G), dim3(kPBlock), 0, s, tiles,
+                           endsT, ntiles, pl, G, words,
                            res);
         phase_end(kPhaseProbeSeg, s);
         phase_begin(kPhaseProbeOut, s);
