@@ -274,7 +274,8 @@ def bench_var(ctx, args):
                    % (n // 10**6, mean_len, args.bits_per_key, m, k, nn // 10**6)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "partitioned build (offsets layout)",
-                     "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_key": bpk},
+                     "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_key": bpk,
+                     "phases": phase_report(phases, args.steps)},
         "probe": {"keys_per_s": nn / (float(np.mean(pkms)) / 1e3), "false_positives": fp,
                   "fpr": fp / nn, "kernel_ms": float(np.mean(pkms)),
                   "ms_by_strategy": time_probe_strategies(ctx, lambda st: call(

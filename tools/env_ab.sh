@@ -15,5 +15,5 @@ for e in ${AB_ENVS}; do
   fi
   env $e timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 ${AB_ARGS:-} > gpurun_out/ab_bench_$i.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/ab_bench_$i.log; exit $rc; }
-  python -c "import json,sys; d=json.loads([l for l in open('gpurun_out/ab_bench_$i.log') if l.startswith('{')][-1]); print(round(d['value']/1e9,2), 'G keys/s', {k: round(v['ms_per_launch'],3) for k,v in d['roofline']['phases'].items()})"
+  python -c "import json,sys; d=json.loads([l for l in open('gpurun_out/ab_bench_$i.log') if l.startswith('{')][-1]); print(round(d['value']/1e9,2), 'G keys/s', {k: round(v['ms_per_launch'],3) for k,v in d['roofline'].get('phases', {}).items()})"
 done

@@ -77,16 +77,35 @@ __device__ __forceinline__ Prefix key_prefix(const DevKeys& a, uint64_t j) {
         Sip st = sip_init();
         if constexpr (LP) sip_compress(st, len);
         const uint64_t nfull = len >> 3;
+        // Source words c+1..c+4 sit in a[] while words c+5..c+8 are already in flight in b[]:
+        // the absorb never waits on a load it just issued (a word past the key reads as 0).
         uint64_t lo = len ? ld_word(wbase, wstart, end, 0) : 0ull;
-        for (uint64_t c = 0; c < nfull; ++c) {
-            const uint64_t hi = ld_word(wbase, wstart, end, c + 1);
-            sip_compress(st, funnel(lo, hi, sh));
-            lo = hi;
+        uint64_t a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = ld_word(wbase, wstart, end, 1 + i);
+        uint64_t c = 0;
+        for (; c + 4 <= nfull; c += 4) {
+            uint64_t b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[i] = ld_word(wbase, wstart, end, c + 5 + i);
+            sip_compress(st, funnel(lo, a[0], sh));
+            sip_compress(st, funnel(a[0], a[1], sh));
+            sip_compress(st, funnel(a[1], a[2], sh));
+            sip_compress(st, funnel(a[2], a[3], sh));
+            lo = a[3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = b[i];
         }
+        // 0..3 full blocks left: words c+1.. are a[0..]; the tail's upper word is a[nfull - c]
+        const uint32_t left = (uint32_t)(nfull - c);
+        uint64_t up = a[0];
+        if (left > 0) { sip_compress(st, funnel(lo, a[0], sh)); lo = a[0]; up = a[1]; }
+        if (left > 1) { sip_compress(st, funnel(lo, a[1], sh)); lo = a[1]; up = a[2]; }
+        if (left > 2) { sip_compress(st, funnel(lo, a[2], sh)); lo = a[2]; up = a[3]; }
         p.st = st;
         p.r = (uint32_t)(len & 7);  // P % 8 == len % 8 (the length block is 8 bytes)
         const uint64_t tmask = p.r ? (~0ull >> (64 - 8 * p.r)) : 0ull;
-        p.tail = p.r ? (funnel(lo, ld_word(wbase, wstart, end, nfull + 1), sh) & tmask) : 0ull;
+        p.tail = p.r ? (funnel(lo, up, sh) & tmask) : 0ull;
         p.total = (uint32_t)((len + (LP ? 8 : 0) + 8) & 0xff);
     }
     return p;

@@ -104,6 +104,37 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
     }
 }
 
+// Variable-length keys (offsets layout): a wave runs the prefix-absorb loop as long as its
+// longest key, and with Zipf lengths almost every wave holds one long key.  So the tile's keys
+// are dealt to lanes in order of length -- a counting sort on min(len / 8, 31) into perm[] in
+// LDS -- and a wave's lanes absorb similar numbers of blocks.  The build is an OR over keys, so
+// the order changes speed only.  hist[kLenBuckets] must be zero on entry; ends with a barrier.
+constexpr int kLenBuckets = 32;
+
+__device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, uint32_t nk, uint16_t* perm,
+                                             uint32_t* hist) {
+    const uint32_t tid = threadIdx.x;
+    auto bucket = [&](uint32_t l) {
+        const uint64_t len = dk.offsets[key0 + l + 1] - dk.offsets[key0 + l];
+        return (uint32_t)std::min<uint64_t>(len >> 3, kLenBuckets - 1);
+    };
+    for (uint32_t l = tid; l < nk; l += kPBlock) atomicAdd(&hist[bucket(l)], 1u);
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t v = tid < kLenBuckets ? hist[tid] : 0u;
+        uint32_t incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (tid >= (uint32_t)o) incl += y;
+        }
+        if (tid < kLenBuckets) hist[tid] = incl - v;
+    }
+    __syncthreads();
+    for (uint32_t l = tid; l < nk; l += kPBlock) perm[atomicAdd(&hist[bucket(l)], 1u)] = (uint16_t)l;
+    __syncthreads();
+}
+
 // K > 0: k known at compile time (the stash and seed loops unroll, no indexed register moves);
 // K == 0: any k <= kStash at run time.
 template <int FMT, bool LP, int K>
@@ -114,6 +145,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     uint32_t* hi = smem + pl.CP / 2;                    // CP/8 words, 8 nibbles each
     uint32_t* cnt = hi + pl.CP / 8;                     // nseg_pad
     uint32_t* wsum = cnt + pl.nseg_pad;                 // 16
+    uint32_t* lhist = wsum + 16;                        // kLenBuckets (offsets layout)
     const uint32_t tid = threadIdx.x;
     // Stagger (speed only): the second workgroup dispatched to each CU starts ~half a tile
     // later, so the two co-resident workgroups alternate hashing (VALU) and sorting (LDS)
@@ -123,20 +155,25 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     }
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
     for (uint32_t w = tid; w < pl.CP / 8; w += kPBlock) hi[w] = 0;
+    if (FMT < 0 && tid < kLenBuckets) lhist[tid] = 0;
     __syncthreads();
 
     uint32_t stash[kStash];
     const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
     const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
+    const uint32_t nk = (uint32_t)(key_end - key0);
+    // perm lives in the (not yet used) tile image; every read of it precedes the barrier below
+    if constexpr (FMT < 0) length_order(dk, key0, nk, lo, lhist);
+    auto key_of = [&](uint32_t slot) -> uint64_t { return key0 + (FMT < 0 ? (uint32_t)lo[slot] : slot); };
     uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     if constexpr (K > 0) {
         constexpr int RM = rounds_max(K);
 #pragma unroll
         for (int r = 0; r < RM; ++r) {
-            const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
-            const bool valid = (uint32_t)r < pl.R && j < key_end;
+            const uint32_t slot = (uint32_t)r * kPBlock + tid;
+            const bool valid = (uint32_t)r < pl.R && slot < nk;
             Prefix p{};
-            if (valid) p = key_prefix<FMT, LP>(dk, j);
+            if (valid) p = key_prefix<FMT, LP>(dk, key_of(slot));
 #pragma unroll
             for (int i = 0; i < K; ++i) {
                 uint32_t idx = kSentinel;
@@ -151,10 +188,10 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     } else {
         ns = 0;
         for (uint32_t r = 0; r < pl.R; ++r) {
-            const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
-            const bool valid = j < key_end;
+            const uint32_t slot = r * kPBlock + tid;
+            const bool valid = slot < nk;
             Prefix p{};
-            if (valid) p = key_prefix<FMT, LP>(dk, j);
+            if (valid) p = key_prefix<FMT, LP>(dk, key_of(slot));
             for (uint32_t i = 0; i < pl.k; ++i) {
                 uint32_t idx = kSentinel;
                 if (valid) {
@@ -493,7 +530,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     const uint32_t rmax = (uint32_t)rounds_max((int)k);
     for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
-        const int64_t avail = (int64_t)budget - 64 - 4 * (int64_t)pl.nseg_pad;
+        const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)pl.nseg_pad;
         // LDS = 2.5 * CP with CP <= C + nseg + 8
         const int64_t cmax = avail * 2 / 5 - pl.nseg - 8;
         const int64_t kt = std::min<int64_t>((int64_t)rmax * kPBlock, cmax / k);
@@ -506,7 +543,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.C = pl.KT * k;
     pl.CP = (pl.C + pl.nseg + 7) & ~7u;
     pl.tile_words = pl.CP / 2 + pl.CP / 8;
-    pl.lds1 = (pl.CP / 2 + pl.CP / 8 + pl.nseg_pad + 16) * 4;
+    pl.lds1 = (pl.CP / 2 + pl.CP / 8 + pl.nseg_pad + 16 + kLenBuckets) * 4;
     // stagger the second resident workgroup per CU by ~half a tile of hashing (~25 us at k=10,
     // ~3000 keys): s_sleep 127 = 8128 cycles, ~3.7 us.  VBF_STAGGER=0 disables (A/B).
     static const int env = [] { const char* e = getenv("VBF_STAGGER"); return e ? atoi(e) : -1; }();
