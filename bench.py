@@ -92,6 +92,15 @@ def timed_steps(ctx, step, steps, warmup):
     Returns (max-over-ranks wall seconds, torch-event ms per step, library phase timings).
     The library brackets each kernel phase with hipEvents on the launch stream."""
     from velarixdb_amd._lib import lib, profile_read
+    # Clock settle (untimed, on top of the W warmup steps): MI355X kernel durations keep
+    # falling for the first ~25 ms of sustained load (k_tile_pack 4.6 -> 3.7 ms over its first
+    # six launches under rocprofv3), so keep stepping until 0.3 s of work has run.
+    t_settle = time.perf_counter()
+    while True:
+        step(None)
+        torch.cuda.synchronize()
+        if time.perf_counter() - t_settle > 0.3:
+            break
     for _ in range(warmup):
         step(None)
     torch.cuda.synchronize()
@@ -198,6 +207,9 @@ def bench_fixed(ctx, args):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "build (all phases of one vbf_build_dev_ex launch)", "kernel_ms": kavg * 1e3,
+                     "rocprof_kernels": {"tile_sort": "k_tile_pack<16, true, 10>", "transpose": "k_transpose_u16",
+                                         "seg_or": "k_seg_or<3, 1024, 5>"},
+                     "rocprof_summary": "profiles/r01/bench_default_kernel_stats.csv",
                      "valu_frac_est": n * VALU_PER_KEY_CFG2 / kavg / VALU_PEAK_LANE_OPS,
                      "algorithmic_bytes_per_key": bytes_per_key,
                      "siprounds_per_key": (L + 8) // 8 + 5 * k,
@@ -515,8 +527,8 @@ def bench_multi(ctx, args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
     ap.add_argument("--keys", type=int, default=None)
     ap.add_argument("--key-bytes", type=int, default=16)
