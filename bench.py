@@ -199,9 +199,10 @@ def bench_fixed(ctx, args):
         "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "key_gib_per_s": value * L / 2**30,
-        "config": {"workload": "config%d: %dM x %dB keys per GPU, %d bits/key (m=%d, k=%d)%s" % (
-            2 if ctx.world == 1 else 4, n // 10**6, L, args.bits_per_key, m, k,
-            "" if ctx.world == 1 else ", one independent SSTable shard per GPU"),
+        "config": {"workload": "config2: %dM x %dB keys per GPU, %d bits/key (m=%d, k=%d)%s" % (
+            n // 10**6, L, args.bits_per_key, m, k,
+            "" if ctx.world == 1 else
+            "; %d independent SSTable shards, one per GPU (config 4's compaction fan-in, weak scaling)" % ctx.world),
             "n_keys_per_gpu": n, "key_bytes": L, "m_bits": m, "k": k, "len_prefix": True,
             "parallelism": "independent shards x%d" % ctx.world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
