@@ -144,6 +144,25 @@ int vbf_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
                    int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint64_t nwords,
                    uint8_t* out, int device);
 
+/* Compaction fan-in (src/compactors/sized.rs:170-200 builds one filter per merged SSTable, each
+ * from its own entries): independent builds spread over devices[0..ndevices), shard s on
+ * devices[s % ndevices], one host thread and its own staging streams per device, shards of one
+ * device in order.  Each shard is a vbf_build_host call: host keys, ORed into its host words.
+ * Per-shard status lands in shards[s].status; the return value is the first failure's (the
+ * message is this thread's vbf_last_error). */
+typedef struct vbf_shard {
+    const uint8_t* keys;
+    const uint64_t* offsets; /* n+1 host offsets, or NULL for fixed `stride` */
+    uint64_t stride;
+    uint64_t n;
+    int len_prefix;
+    uint32_t m, k;
+    uint32_t* words;         /* host, ceil(m/32) words, OR-accumulated */
+    uint64_t nwords;
+    int status;              /* out */
+} vbf_shard;
+int vbf_build_shards_host(vbf_shard* shards, uint64_t nshards, const int* devices, int ndevices);
+
 /* ---- BloomFilter handle: the bit array lives in HBM on `device` ---- */
 typedef struct vbf_filter vbf_filter;
 

@@ -148,3 +148,14 @@ def test_filter_file_extension_roundtrip():
     assert filter_file.decode(ref) == (19, 1791, 1e-4, None, None)
     with pytest.raises(EOFError):
         filter_file.decode(ref[:12])
+
+
+def test_shard_build_argument_checks():
+    """vbf_build_shards_host validates before touching a device (no kernel launched)."""
+    from velarixdb_amd._lib import VBF_EINVAL, VBF_OK, lib
+    from velarixdb_amd.compaction import _Shard
+    assert lib.vbf_build_shards_host(None, 0, None, 0) == VBF_OK
+    shards = (_Shard * 1)()
+    assert lib.vbf_build_shards_host(ctypes.cast(shards, ctypes.c_void_p), 1, None, 0) == VBF_EINVAL
+    assert b"no devices" in lib.vbf_last_error()
+    assert lib.vbf_build_shards_host(None, 3, None, 1) == VBF_EINVAL

@@ -170,3 +170,30 @@ def test_large_merge_and_device_gather(vbf, ora):
     bf.set_dev(P(ok_), P(oo), 0, n.value, 1)
     assert np.array_equal(bf.words(), ora.build_words(vbf.pack_fixed(wk.reshape(-1, 16)), bf.num_bits(),
                                                       bf.no_of_hash_func, threads=8))
+
+
+def test_sharded_filter_builds(vbf, ora):
+    """The compaction fan-in's independent per-table builds (vbf_build_shards_host): every
+    shard's words equal the oracle's, whatever thread/device serves it; an unusable device fails
+    that shard only and the call reports it."""
+    from velarixdb_amd.compaction import _Shard, build_filters_sharded
+    from velarixdb_amd.keys import pack, pack_fixed
+    rng = np.random.default_rng(11)
+    batches = [pack_fixed(rng.integers(0, 256, (20_000, 16), dtype=np.uint8)),
+               pack([bytes(rng.integers(0, 256, int(n), dtype=np.uint8)) for n in rng.integers(0, 90, 5_000)]),
+               pack_fixed(rng.integers(0, 256, (1, 32), dtype=np.uint8)),
+               pack_fixed(rng.integers(0, 256, (70_000, 8), dtype=np.uint8))]
+    for devices in ((0,), (0, 0, 0)):
+        got = build_filters_sharded(batches, 0.01, devices)
+        for b, (m, k, words) in zip(batches, got):
+            assert np.array_equal(words, ora.build_words(b, m, k)), (devices, b.n)
+    b = batches[0]
+    words = np.zeros(100, np.uint32)
+    d, o = b.ptrs()
+    shards = (_Shard * 2)(_Shard(d, o, b.stride, b.n, 1, 3200, 3, words.ctypes.data, 100, 0),
+                          _Shard(d, o, b.stride, b.n, 1, 3200, 3, words.ctypes.data, 100, 0))
+    devs = (ctypes.c_int * 2)(0, 99)
+    rc = vbf.lib.vbf_build_shards_host(ctypes.cast(shards, ctypes.c_void_p), 2, ctypes.cast(devs, ctypes.c_void_p), 2)
+    assert rc == vbf._lib.VBF_ENODEV and shards[0].status == 0 and shards[1].status == vbf._lib.VBF_ENODEV
+    assert b"shard 1" in vbf.lib.vbf_last_error()
+    assert np.array_equal(words, ora.build_words(b, 3200, 3))

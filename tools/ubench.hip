@@ -146,10 +146,40 @@ __device__ __forceinline__ uint32_t fmod_(uint64_t x, uint64_t m, uint64_t mu) {
     return (uint32_t)r;
 }
 
+// Exact x % m for 2^13 <= m < 2^32 with one 32-bit multiply: an f64 estimate of the quotient
+// (off by at most one), the remainder's low word in integers, and the f64 remainder estimate
+// (error <= 2^10) to tell which multiple of 2^32 the low word stands for.
+__device__ __forceinline__ uint32_t fmod_f64(uint64_t x, uint32_t m, double inv_m, double m_f) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const double xf = __fma_rn((double)xh, 4294967296.0, (double)xl);
+    const double qf = floor(xf * inv_m);
+    const double qh = floor(qf * (1.0 / 4294967296.0));
+    const uint32_t ql = (uint32_t)__fma_rn(-qh, 4294967296.0, qf);
+    const uint32_t rl = xl - ql * m;
+    const double d = __fma_rn(-qf, m_f, xf) - (double)rl;
+    uint32_t r = rl;
+    if (d < -2147483648.0) r = rl + m;
+    else if (d > 2147483648.0 || rl >= m) r = rl - m;
+    return r;
+}
+
+__global__ void k_mod_check(uint64_t n, uint64_t m, uint64_t mu, double inv_m, unsigned long long* bad) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n) return;
+    uint64_t x = j * 0x9E3779B97F4A7C15ULL;
+    x ^= x >> 29; x *= 0xBF58476D1CE4E5B9ULL; x ^= x >> 32;
+    if ((j & 7) == 0) x = ~0ull - (j >> 3);              // near 2^64
+    if ((j & 7) == 1) x = (j >> 3) * m + (j & 0xff) - 128;  // near multiples of m
+    const uint32_t a = (uint32_t)(x % m);
+    const uint32_t b = fmod_f64(x, (uint32_t)m, inv_m, (double)m);
+    if (a != b) atomicAdd(bad, 1ull);
+}
+
 // MODE: 0 = V1 hash only; 1 = V1 + mod; 2 = V1, two seeds interleaved, + mod; 3 = V3 + mod;
 // 5 = V5 (swap folded into carry adds) + mod
 template <int MODE, int BS>
 __global__ __launch_bounds__(BS) void k_hash2(uint64_t n, int k, uint64_t m, uint64_t mu, uint64_t* out) {
+    const double inv_m = 1.0 / (double)m;
     extern __shared__ uint32_t pad[];
     uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
     if (j >= n) return;
@@ -174,7 +204,9 @@ __global__ __launch_bounds__(BS) void k_hash2(uint64_t n, int k, uint64_t m, uin
             S t = s;
             comp<V>(t, (uint32_t)i);
             const uint64_t h = fin<V>(t, 32ull << 56);
-            if constexpr (MODE == 0) acc ^= h; else acc += fmod_(h, m, mu);
+            if constexpr (MODE == 0) acc ^= h;
+            else if constexpr (MODE == 8) acc += fmod_f64(h, (uint32_t)m, inv_m, (double)m);
+            else acc += fmod_(h, m, mu);
         }
     }
     if (acc == 0x123456789ull) out[0] = acc + pad[0];
@@ -322,6 +354,22 @@ int main(int argc, char** argv) {
         run(k_hash2<2, 256>, 256, 0, "V1 2-seed interleave + mod, 256 thr");
         run(k_hash2<3, 256>, 256, 0, "V3 addc + mod, 256 thr");
         run(k_hash2<5, 256>, 256, 0, "V5 swap-folded carry adds + mod, 256 thr");
+        run(k_hash2<8, 256>, 256, 0, "V1 + f64-estimate mod, 256 thr");
+        run(k_hash2<8, 1024>, 1024, 80 * 1024, "V1 + f64-estimate mod, 1024 thr, 2 blocks/CU");
+        {
+            unsigned long long* bad;
+            CHECK(hipMalloc(&bad, 8));
+            for (uint64_t mm : {8192ull, 8193ull, 1000000000ull, 2147483647ull, 2147483648ull, 3000000019ull,
+                                4294967295ull, 4294967291ull, 123457ull, 10000000ull}) {
+                CHECK(hipMemset(bad, 0, 8));
+                const uint64_t nn = 1ull << 26;
+                hipLaunchKernelGGL(k_mod_check, dim3((unsigned)(nn / 256)), dim3(256), 0, 0, nn, mm, ~0ull / mm,
+                                   1.0 / (double)mm, bad);
+                unsigned long long hb = 0;
+                CHECK(hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost));
+                printf("  fmod_f64 exactness m=%llu: %llu mismatches in 2^26\n", (unsigned long long)mm, hb);
+            }
+        }
         run(k_hash2<6, 256>, 256, 0, "V6 pk_mov swap + mod, 256 thr");
         run(k_hash2<7, 256>, 256, 0, "V6 pk_mov swap, 2-seed + mod, 256 thr");
         run(k_hash2<6, 1024>, 1024, 80 * 1024, "V6 pk_mov swap + mod, 1024 thr, 2 blocks/CU");

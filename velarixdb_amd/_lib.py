@@ -56,6 +56,7 @@ SIGNATURES = {
     "vbf_gen_var_dev": (_int, [_u64, _u64, _u64, _vp, _vp, _vp]),
     "vbf_build_host": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _u64, _int]),
     "vbf_probe_host": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _u64, _vp, _int]),
+    "vbf_build_shards_host": (_int, [_vp, _u64, _vp, _int]),
     "vbf_filter_new": (_int, [_dbl, _u64, _int, ctypes.POINTER(_vp)]),
     "vbf_filter_default": (_int, [_int, ctypes.POINTER(_vp)]),
     "vbf_filter_recover": (_int, [_vp, ctypes.c_size_t, _int, ctypes.POINTER(_vp)]),
@@ -103,6 +104,14 @@ def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError("velarixdb_amd: %s is missing; run __graft_entry__.build() "
                           "(hipcc --offload-arch=gfx950). There is no CPU fallback." % LIB_PATH)
+    # One HIP runtime per process.  libvbf.so needs libamdhip64.so.7; PyTorch-ROCm ships its own
+    # copy under that soname.  Loaded after torch, libvbf binds to torch's copy; loaded first,
+    # it pulls in /opt/rocm's and a later `import torch` binds to that one and finds no GPU.
+    # So when torch is installed it is imported (not initialised) first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -9,6 +9,8 @@ Mirrors the merge half of SizedTierRunner (src/compactors/sized.rs):
                                                    with tombstone_check (:286-320), then
                                                    BloomFilter::new(p, n) + build (:192-193)
   .clear_tombstones()                           run_compaction's clear when nothing is left (:73-75)
+  build_filters_sharded(batches, p, devices)    the fan-in's per-table filter builds (:192-193 for
+                                                   every merged table), one table per device
 
 The fold runs on the device (C ABI vbf_compact_merge_host); it returns the merged entries as
 ids into the input tables -- what a Rust caller maps back onto its own Entry values -- and the
@@ -104,3 +106,32 @@ class SizedTierMerger:
         bf = BloomFilter(self.config.filter_false_positive, len(merged), device=self.device)
         bf.set_batch(pack_offsets(merged.keys, merged.offsets))
         return merged, bf
+
+
+class _Shard(ctypes.Structure):
+    """struct vbf_shard (include/vbf.h)."""
+    _fields_ = [("keys", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("stride", ctypes.c_uint64),
+                ("n", ctypes.c_uint64), ("len_prefix", ctypes.c_int), ("m", ctypes.c_uint32),
+                ("k", ctypes.c_uint32), ("words", ctypes.c_void_p), ("nwords", ctypes.c_uint64),
+                ("status", ctypes.c_int)]
+
+
+def build_filters_sharded(batches, false_positive_rate=DEFAULT_FALSE_POSITIVE_RATE, devices=(0,)):
+    """Independent filter builds for the tables a compaction produced (sized.rs:192-193, once
+    per merged table), spread over `devices` with one host thread per device
+    (vbf_build_shards_host).  batches: HostBatch per table.  Returns a list of
+    (m, k, words) with words the host bit array (bit-vec BitVec<u32> layout)."""
+    from .filter import num_bits, num_hash_functions
+    out, shards, keep = [], (_Shard * max(1, len(batches)))(), []
+    for i, b in enumerate(batches):
+        m = num_bits(max(b.n, 1), false_positive_rate)
+        k = num_hash_functions(m, max(b.n, 1))
+        words = np.zeros((m + 31) // 32, np.uint32)
+        d, o = b.ptrs()
+        shards[i] = _Shard(d, o, b.stride, b.n, b.len_prefix, m, k, words.ctypes.data, words.size, 0)
+        out.append((m, k, words))
+        keep.append(b)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    call("vbf_build_shards_host", ctypes.cast(shards, ctypes.c_void_p), len(batches), ctypes.cast(devs, ctypes.c_void_p),
+         len(devices))
+    return out

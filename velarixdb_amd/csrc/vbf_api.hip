@@ -895,6 +895,29 @@ int vbf_build_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
     return ok();
 }
 
+int vbf_build_shards_host(vbf_shard* shards, uint64_t nshards, const int* devices, int ndevices) {
+    if (nshards && !shards) return fail(VBF_EINVAL, "shards is NULL");
+    if (nshards && (!devices || ndevices <= 0)) return fail(VBF_EINVAL, "no devices given");
+    std::vector<std::string> msg(nshards);
+    auto work = [&](int d) {
+        for (uint64_t s = (uint64_t)d; s < nshards; s += (uint64_t)ndevices) {
+            vbf_shard& sh = shards[s];
+            sh.status = vbf_build_host(sh.keys, sh.offsets, sh.stride, sh.n, sh.len_prefix, sh.m, sh.k, sh.words,
+                                       sh.nwords, devices[d]);
+            if (sh.status) msg[s] = g_err;
+        }
+    };
+    const int nt = (int)std::min<uint64_t>((uint64_t)ndevices, nshards);
+    std::vector<std::thread> th;
+    th.reserve(nt > 0 ? nt - 1 : 0);
+    for (int d = 1; d < nt; ++d) th.emplace_back(work, d);
+    if (nt > 0) work(0);
+    for (auto& t : th) t.join();
+    for (uint64_t s = 0; s < nshards; ++s)
+        if (shards[s].status) return fail(shards[s].status, "shard %llu: %s", (unsigned long long)s, msg[s].c_str());
+    return ok();
+}
+
 int vbf_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                    int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint64_t nwords,
                    uint8_t* out, int device) {
