@@ -52,5 +52,18 @@ def build(force=False, verbose=False):
     return OUT
 
 
+def build_examples(verbose=False):
+    """examples/c_host: the C ABI from a plain C host (gcc, no Python/torch in that process)."""
+    root = os.path.dirname(HERE)
+    src = os.path.join(root, "examples", "c_host.c")
+    out = os.path.join(root, "examples", "c_host")
+    cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-I", os.path.join(root, "include"), src,
+           "-L", HERE, "-lvbf", "-Wl,-rpath,$ORIGIN/../velarixdb_amd", "-o", out]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd)
+    return out
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
