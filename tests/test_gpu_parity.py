@@ -371,3 +371,26 @@ def test_filter_db_persisted_bits(vbf, tmp_path):
     r2 = BloomFilter.default()
     r2.file_path = mem.file_path
     assert r2.recover_meta() is False and not r2.words().any()
+
+
+def test_product_library_ignores_ablation_env(vbf, tmp_path):
+    """VBF_ABLATE (timing experiments that skip phases) only acts in the separate ablation build
+    (vbf_kernels.hpp); the product libvbf.so must build correct filters with it set."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import numpy as np, oracle, velarixdb_amd as v\n"
+        "from velarixdb_amd.keys import pack_fixed\n"
+        "b = pack_fixed(np.random.default_rng(3).integers(0, 256, (300000, 16), dtype=np.uint8))\n"
+        "m, k = 3_000_000, 10\n"
+        "w = np.zeros((m + 31) // 32, np.uint32)\n"
+        "v._lib.call('vbf_build_host', b.data.ctypes.data, None, 16, b.n, 1, m, k, w.ctypes.data, w.size, 0)\n"
+        "assert np.array_equal(w, oracle.build_words(b, m, k)), 'ablation env changed the product build'\n"
+        "print('ok')\n" % ROOT)
+    env = {kk: vv for kk, vv in os.environ.items() if kk != "VBF_LIB"}
+    for a in ("1", "4", "7"):
+        env["VBF_ABLATE"] = a
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "ok" in r.stdout, (a, r.stderr[-2000:])

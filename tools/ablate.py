@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """Phase ablation of the partitioned build (timing only; results are wrong with VBF_ABLATE>0).
 
+Needs the ablation build of the library (the product libvbf.so ignores VBF_ABLATE):
+`python velarixdb_amd/build.py --ablation` writes velarixdb_amd/libvbf_ablate.so, which the
+children load through VBF_LIB.
+
 Runs the config-2 build in child processes with VBF_ABLATE=0/1/2 and prints the library's
 per-phase hipEvent timings: 0 = full build, 1 = hash + count + scan (no place/copy),
 2 = hash only (no LDS count either), 3 = seg_or loads without ds_or, 4 = seg_or ds_or on
@@ -37,7 +41,10 @@ print(json.dumps({p: round(ms / max(c, 1), 3) for p, (ms, c) in ph.items() if c}
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for a in ("0", "1", "2", "3", "4", "5", "6", "7"):
-    env = dict(os.environ, VBF_ABLATE=a, ROOT=root)
+    lib = os.path.join(root, "velarixdb_amd", "libvbf_ablate.so")  # build.py --ablation
+    if not os.path.exists(lib):
+        sys.exit("missing %s: run `python velarixdb_amd/build.py --ablation` first" % lib)
+    env = dict(os.environ, VBF_ABLATE=a, ROOT=root, VBF_LIB=lib)
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
     print("VBF_ABLATE=%s" % a, line[-1] if line else out.stderr[-2000:], flush=True)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Timing ablation of the data.db walk (results are wrong with VBF_ABLATE set):
+"""Timing ablation of the data.db walk (results are wrong with VBF_ABLATE set; needs the
+ablation build velarixdb_amd/libvbf_ablate.so from `python velarixdb_amd/build.py --ablation`):
 0 = full, 11 = staging only (no walk), 12 = synthetic 124-step walk without staging,
 13 = dependent 124-step LDS chain without staging, 14 = staging + that chain."""
 import os
@@ -35,7 +36,10 @@ print(json.dumps({p: round(ms / max(c, 1), 3) for p, (ms, c) in ph.items() if c}
 """
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for a in ("0", "11", "12", "13", "14"):
-    env = dict(os.environ, VBF_ABLATE=a, ROOT=root)
+    lib = os.path.join(root, "velarixdb_amd", "libvbf_ablate.so")  # build.py --ablation
+    if not os.path.exists(lib):
+        sys.exit("missing %s: run `python velarixdb_amd/build.py --ablation` first" % lib)
+    env = dict(os.environ, VBF_ABLATE=a, ROOT=root, VBF_LIB=lib)
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=240)
     line = [l for l in out.stdout.splitlines() if l.startswith("{")]
     print("VBF_ABLATE=%s %s" % (a, line[0] if line else out.stderr[-500:]), flush=True)

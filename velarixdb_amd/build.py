@@ -26,13 +26,16 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=False):
-    """One hipcc per translation unit, in parallel, then one link."""
-    if not force and not needs_build():
+def build(force=False, verbose=False, out=OUT, defines=()):
+    """One hipcc per translation unit, in parallel, then one link.  `defines` (e.g.
+    VBF_ABLATION_BUILD=1 for tools/ablate.py, written to velarixdb_amd/libvbf_ablate.so) build a
+    variant library for VBF_LIB; the product is libvbf.so without any."""
+    if out == OUT and not defines and not force and not needs_build():
         return OUT
-    objdir = os.path.join(HERE, "..", "build", "obj")
+    tag = "_".join(d.replace("=", "") for d in defines)
+    objdir = os.path.join(HERE, "..", "build", "obj" + ("_" + tag if tag else ""))
     os.makedirs(objdir, exist_ok=True)
-    flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++20", "-fPIC", "-Wall"]
+    flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++20", "-fPIC", "-Wall"] + ["-D" + d for d in defines]
     procs, objs = [], []
     for s in SOURCES:
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
@@ -44,12 +47,12 @@ def build(force=False, verbose=False):
     failed = [s for s, p in procs if p.wait() != 0]
     if failed:
         raise RuntimeError("hipcc failed for " + ", ".join(failed))
-    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.check_call(cmd, cwd=CSRC)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 def build_examples(verbose=False):
@@ -65,5 +68,10 @@ def build_examples(verbose=False):
     return out
 
 
+ABLATION_LIB = os.path.join(HERE, "libvbf_ablate.so")
+
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if "--ablation" in sys.argv:
+        print(build(verbose=True, out=ABLATION_LIB, defines=("VBF_ABLATION_BUILD=1",)))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

@@ -1,5 +1,12 @@
 // vbf_kernels.hpp -- internal launch interface between the C ABI (vbf_api.hip) and the kernels.
 #pragma once
+
+// Ablation builds (timing experiments, tools/ablate*.py): compiled with -DVBF_ABLATION_BUILD=1 and
+// loaded through VBF_LIB, they honour VBF_ABLATE, which skips phases and so gives WRONG
+// results.  The product library is built without it and ignores VBF_ABLATE.
+#ifndef VBF_ABLATION_BUILD
+#define VBF_ABLATION_BUILD 0
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -74,7 +81,7 @@ struct SstArgs {
     uint64_t* created;
     uint8_t* tomb;
     uint32_t* err;           // [0] error bits, [1] first bad block, [2]/[3] min/max key length
-    uint32_t ablate;         // timing experiments only (VBF_ABLATE 11/12)
+    uint32_t ablate;         // timing experiments only (VBF_ABLATE 11-14, ablation builds)
 };
 hipError_t sst_count(const SstArgs& a, hipStream_t s);
 hipError_t sst_emit(const SstArgs& a, hipStream_t s);

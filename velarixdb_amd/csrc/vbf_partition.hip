@@ -60,7 +60,7 @@ struct PartPlan {
     uint32_t tile_words;  // u32 words per tile in the workspace: CP/2 (lo16) + CP/8 (nibbles)
     uint32_t lds1;        // K1 dynamic LDS bytes
     uint32_t stagger_lo, stagger_hi, stagger_sleeps;
-    uint32_t ablate;      // timing experiments only (VBF_ABLATE): 1 skip place+copy, 2 also count
+    uint32_t ablate;      // ablation builds only (VBF_ABLATE, vbf_kernels.hpp): 1 skip place+copy
     uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or)
     uint64_t m, mu, nwords;
 };
@@ -551,7 +551,10 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.stagger_lo = 256;
     pl.stagger_hi = 512;
     pl.stagger_sleeps = sleeps;
-    static const int abl = [] { const char* e = getenv("VBF_ABLATE"); return e ? atoi(e) : 0; }();
+    static const int abl = [] {
+        const char* e = VBF_ABLATION_BUILD ? getenv("VBF_ABLATE") : nullptr;  // vbf_kernels.hpp
+        return e ? atoi(e) : 0;
+    }();
     pl.ablate = (uint32_t)abl;
     static const int k3v = [] { const char* e = getenv("VBF_K3"); return e ? atoi(e) : 4; }();
     pl.k3v = (uint32_t)k3v;
