@@ -28,7 +28,6 @@
 namespace vbf {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr int kMergeIpt = 4;  // outputs per lane per merge level
 
 // Rust `Ord for [u8]` on two keys of the arena: 8 bytes at a time as big-endian words (global
 // memory takes unaligned 8-byte loads), then the tail byte by byte.

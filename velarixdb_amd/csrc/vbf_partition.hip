@@ -214,8 +214,11 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
         return;
     }
     // rank + place, 8 returning LDS atomics in flight before their results are used
+    // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
+    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(rounds_max(K) * K) : (uint32_t)kStash;
 #pragma unroll
-    for (uint32_t t = 0; t < ns; t += 8) {
+    for (uint32_t t = 0; t < kNsMax; t += 8) {
+        if (t >= ns) break;
         uint32_t pos[8], val[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -304,12 +307,15 @@ __device__ __forceinline__ void load8(const uint32_t* tile, uint32_t cp, uint32_
 
 // K3 tile-loop variants (VBF_K3, speed only; identical results):
 //   0: two-stage -- run bounds of batch b+1 (8 u16 loads per lane) in flight with batch b's data
-//   2: two-stage, bounds loaded coalesced (one u16 per lane for the wave's 64 tiles) and handed
-//      to the 8-lane groups with ds_bpermute
-//   3: three-stage -- bounds of b+2, data of b+1 and the ORs of b overlap; data loads are
-//      unconditional (idle lanes re-read their run's first 8 entries) so vmcnt waits stay exact;
-//      NG runs per 8-lane group per batch (3: 1024 threads NG=4; 4: 1024, NG=5; 5: 768, NG=6;
-//      6: 768, NG=8)
+//   3: three-stage -- bounds of b+2, data of b+1 and the ORs of b overlap; run bounds loaded
+//      coalesced (one u16 pair per lane for the wave's tiles) and handed to the 8-lane groups with
+//      ds_bpermute; data loads unconditional (idle lanes re-read their run's first 8 entries) so
+//      vmcnt waits stay exact; NG runs per 8-lane group per batch (VBF_K3 3: 1024 threads NG=4;
+//      4 (default): 1024, NG=5; 5: 768, NG=6; 6: 768, NG=8).
+//   Measured and dropped (tools/env_ab.sh): coalesced bounds in the two-stage loop (-3 %);
+//   "flattened" chunks -- a wave's runs cut into 8-entry chunks dealt to lanes back to back,
+//   found by binary search over the chunk prefix, so no lane idles -- 1.03-1.05 ms alone or
+//   three-stage, vs 0.95 ms: the idle lanes' duplicate loads are not what bounds the kernel.
 template <int V, int BS = kPBlock, int NG = 8>
 __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint16_t* endsT,
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
@@ -423,32 +429,6 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
             tg += step;
             if (!more2) break;
             v1 = v2;
-        }
-    } else if constexpr (V == 2) {
-        uint32_t v = lb(tg);
-        while (tg < t_hi) {
-            uint32_t be[8];
-            uint4 l[8];
-            uint32_t nib[8];
-#pragma unroll
-            for (int g = 0; g < 8; ++g) be[g] = (uint32_t)__shfl((int)v, g * 8 + grp);
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                const uint32_t st = be[g] & 0xFFFFu, len = (be[g] >> 16) - st;
-                if (q8 < len) load8(tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words, pl.CP, st + q8, l[g], nib[g]);
-            }
-            v = lb(tg + step);
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                const uint32_t st = be[g] & 0xFFFFu, len = (be[g] >> 16) - st;
-                if (q8 < len) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len - q8));
-            }
-#pragma unroll
-            for (int g = 0; g < 8; ++g) {
-                const uint32_t st = be[g] & 0xFFFFu, len = (be[g] >> 16) - st;
-                if (len > 64) tail(tg + g * 8 + grp, st, len);
-            }
-            tg += step;
         }
     } else {
         // Two-stage pipeline over the wave's 64-tile batches: the run bounds of batch b+1 and the
@@ -627,7 +607,6 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                 : pl.k3v == 4 ? k_seg_or<3, kPBlock, 5>
                 : pl.k3v == 5 ? k_seg_or<3, 768, 6>
                 : pl.k3v == 6 ? k_seg_or<3, 768, 8>
-                : pl.k3v == 2 ? k_seg_or<2>
                               : k_seg_or<0>;
         const int bs = (pl.k3v == 5 || pl.k3v == 6) ? 768 : kPBlock;
         hipLaunchKernelGGL(k3, dim3(pl.nseg * pl.G), dim3(bs), 0, s, tiles, endsT, ntiles, pl, merge, words);
@@ -717,8 +696,11 @@ __global__ __launch_bounds__(kPBlock) void k_probe_pack(DevKeys dk, ProbePlan pl
     block_exclusive_scan(pst, pl.nseg, wsum);
     __syncthreads();
     const uint32_t per = K > 0 ? (uint32_t)K : pl.k;
+    // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
+    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(rounds_max(K) * K) : (uint32_t)kStash;
 #pragma unroll
-    for (uint32_t t = 0; t < ns; t += 8) {
+    for (uint32_t t = 0; t < kNsMax; t += 8) {
+        if (t >= ns) break;
         uint32_t pos[8], val[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {

@@ -144,7 +144,13 @@ __device__ __forceinline__ uint32_t walk_chain(const BlockView& v, uint32_t blen
             } else {
                 L = blen - p >= 4 ? __builtin_amdgcn_readfirstlane(v.u32(p)) : 0x10000u;
             }
+            // Lane select through m0: two SGPR operands would break gfx9's one-read constant bus.
+            // Nothing in this file depends on m0 across the statement (no LDS-DMA, no sendmsg),
+            // so the reserved-register clobber LLVM warns about is safe here.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
             asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(pr[k]) : "s"(p), "s"(i) : "m0");
+#pragma clang diagnostic pop
             p = L > 0xFFFFu ? 0x20000u : p + L + kEntryFixed;
             lmin = std::min(lmin, L);
             lmax = std::max(lmax, L);
