@@ -394,3 +394,31 @@ def test_product_library_ignores_ablation_env(vbf, tmp_path):
         env["VBF_ABLATE"] = a
         r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0 and "ok" in r.stdout, (a, r.stderr[-2000:])
+
+
+@pytest.mark.parametrize("strategy", [1, 2])
+def test_concentrated_indices(vbf, ora, strategy):
+    """Adversarial skew: 3M copies of three keys put every tile's 30K bit indices into a handful of
+    segments (runs of thousands, the tail loops of k_seg_or / k_probe_seg), alongside one
+    ordinary key.  Words and probe answers (both probe strategies) must still be exact."""
+    from velarixdb_amd.keys import pack_fixed
+    rng = np.random.default_rng(21)
+    base = rng.integers(0, 256, (4, 16), dtype=np.uint8)
+    rows = np.repeat(base[:3], 1_000_000, axis=0)
+    rows = np.concatenate([rows, base[3:]])
+    b = pack_fixed(rows)
+    m, k = 1_000_000_000, 10
+    got = gpu_build(vbf, b, m, k, strategy=strategy)
+    want = ora.build_words(pack_fixed(base), m, k)
+    assert np.array_equal(got, want)
+    assert int(np.unpackbits(got.view(np.uint8)).sum()) <= 40
+    keys, offs = dev_batch(b)
+    w = _dev(got.view(np.int32))
+    for ps in (1, 2):
+        cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+        vbf._lib.call("vbf_probe_count_dev_ex", _ptr(keys), _ptr(offs), b.stride, b.n, b.len_prefix, m, k,
+                      _ptr(w), _ptr(cnt), ps, _stream())
+        torch.cuda.synchronize()
+        assert int(cnt.item()) == b.n, ps
+    neg = pack_fixed(rng.integers(0, 256, (200_000, 16), dtype=np.uint8))
+    assert not gpu_probe(vbf, neg, m, k, got).any()  # 40 bits of 1e9: no false positive expected
