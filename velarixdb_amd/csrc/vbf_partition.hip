@@ -313,6 +313,8 @@ __device__ __forceinline__ void load8(const uint32_t* tile, uint32_t cp, uint32_
 //      vmcnt waits stay exact; NG runs per 8-lane group per batch (VBF_K3 3: 1024 threads NG=4;
 //      4 (default): 1024, NG=5; 5: 768, NG=6; 6: 768, NG=8).
 //   Measured and dropped (tools/env_ab.sh): coalesced bounds in the two-stage loop (-3 %);
+//   raw buffer loads with out-of-range offsets for idle lanes (no duplicate requests): 0.92 ms,
+//   the same as the duplicates (the texture addresser coalesces them);
 //   "flattened" chunks -- a wave's runs cut into 8-entry chunks dealt to lanes back to back,
 //   found by binary search over the chunk prefix, so no lane idles -- 1.03-1.05 ms alone or
 //   three-stage, vs 0.95 ms: the idle lanes' duplicate loads are not what bounds the kernel.
