@@ -122,3 +122,20 @@ def test_config5_sizing_slice(vbf, ora):
     assert count(vbf, keys, None, L, n, m, k, w_part) == n
     fill = popcount(vbf, w_part) / m
     assert abs(fill - (1 - math.exp(-k * n / m))) < 1e-3
+
+
+def test_multi_chunk_partitioned_paths(vbf):
+    """More than kPartChunkIdx (2^30) bit indices in one call: the partitioned build and the
+    partitioned probe process the batch in chunks.  The chunked build must equal the per-key
+    atomic build bit for bit, and both probe strategies must find every key."""
+    from velarixdb_amd.workloads import SEED_CFG2
+    n, L, m, k = 120_000_000, 16, 1_200_000_000, 10  # 1.2e9 indices -> two chunks
+    keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG2 ^ 0x77, 0, n, L, vp(keys), sp())
+    w_part = build(vbf, keys, None, L, n, m, k, 2)
+    w_atom = build(vbf, keys, None, L, n, m, k, 1)
+    assert torch.equal(w_part, w_atom)
+    for strat in (1, 2):
+        c = torch.zeros(1, dtype=torch.int64, device=DEV)
+        vbf._lib.call("vbf_probe_count_dev_ex", vp(keys), None, L, n, 1, m, k, vp(w_part), vp(c), strat, sp())
+        assert int(c.item()) == n, strat
