@@ -33,33 +33,52 @@ __device__ __forceinline__ uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t sh
     return (lo >> sh) | ((hi << 1) << (63 - sh));
 }
 
+// Fixed-length rows (FMT > 0): the row's words, loaded apart from the absorb so a caller can
+// issue several rows' loads before hashing any of them.
+template <int FMT>
+struct FixedWords {
+    static_assert(FMT > 0 && FMT % 8 == 0, "fixed fast path needs whole 8-byte words");
+    uint64_t w[FMT / 8];
+};
+
+template <int FMT>
+__device__ __forceinline__ FixedWords<FMT> load_fixed(const DevKeys& a, uint64_t j) {
+    constexpr uint32_t NW = FMT / 8;
+    FixedWords<FMT> kw;
+    const uint8_t* kp = a.keys + j * FMT;
+    if constexpr (NW % 2 == 0) {
+#pragma unroll
+        for (uint32_t c = 0; c < NW; c += 2) {
+            const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(kp + 8 * c);
+            kw.w[c] = v.x;
+            kw.w[c + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t c = 0; c < NW; ++c) kw.w[c] = *reinterpret_cast<const uint64_t*>(kp + 8 * c);
+    }
+    return kw;
+}
+
+template <int FMT, bool LP>
+__device__ __forceinline__ Prefix absorb_fixed(const FixedWords<FMT>& kw) {
+    Prefix p;
+    Sip st = sip_init();
+    if constexpr (LP) sip_compress(st, (uint64_t)FMT);
+#pragma unroll
+    for (uint32_t c = 0; c < FMT / 8; ++c) sip_compress(st, kw.w[c]);
+    p.st = st;
+    p.tail = 0;
+    p.r = 0;
+    p.total = (FMT + (LP ? 8 : 0) + 8) & 0xff;
+    return p;
+}
+
 template <int FMT, bool LP>
 __device__ __forceinline__ Prefix key_prefix(const DevKeys& a, uint64_t j) {
     Prefix p;
     if constexpr (FMT > 0) {
-        static_assert(FMT % 8 == 0, "fixed fast path needs whole 8-byte words");
-        constexpr uint32_t NW = FMT / 8;
-        uint64_t w[NW];
-        const uint8_t* kp = a.keys + j * FMT;
-        if constexpr (NW % 2 == 0) {
-#pragma unroll
-            for (uint32_t c = 0; c < NW; c += 2) {
-                const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(kp + 8 * c);
-                w[c] = v.x;
-                w[c + 1] = v.y;
-            }
-        } else {
-#pragma unroll
-            for (uint32_t c = 0; c < NW; ++c) w[c] = *reinterpret_cast<const uint64_t*>(kp + 8 * c);
-        }
-        Sip st = sip_init();
-        if constexpr (LP) sip_compress(st, (uint64_t)FMT);
-#pragma unroll
-        for (uint32_t c = 0; c < NW; ++c) sip_compress(st, w[c]);
-        p.st = st;
-        p.tail = 0;
-        p.r = 0;
-        p.total = (FMT + (LP ? 8 : 0) + 8) & 0xff;
+        p = absorb_fixed<FMT, LP>(load_fixed<FMT>(a, j));
     } else {
         uint64_t beg, len;
         if constexpr (FMT < 0) {
