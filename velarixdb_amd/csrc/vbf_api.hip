@@ -588,6 +588,10 @@ int sst_count_pass(const uint8_t* data, uint64_t len, const uint32_t* blocks, ui
     HIP_TRY(hipMemsetAsync(err, 0, 4, s));
     HIP_TRY(hipMemsetAsync(err + 1, 0xFF, 12, s));
     uint16_t* pos = reinterpret_cast<uint16_t*>(base + o_pos);
+    static const uint32_t walk_v = [] {  // VBF_SST_WALK=0: the scalar entry walk (A/B)
+        const char* e = getenv("VBF_SST_WALK");
+        return e ? (uint32_t)(atoi(e) != 0) : 1u;
+    }();
     static const uint32_t abl = [] {
         const char* e = VBF_ABLATION_BUILD ? getenv("VBF_ABLATE") : nullptr;
         return e ? (uint32_t)atoi(e) : 0u;
@@ -595,7 +599,7 @@ int sst_count_pass(const uint8_t* data, uint64_t len, const uint32_t* blocks, ui
     uint32_t* lmin = reinterpret_cast<uint32_t*>(base + o_lmin);
     uint32_t* lmax = reinterpret_cast<uint32_t*>(base + o_lmax);
     *a = vbf::SstArgs{data, len, blocks, nblocks, counts, pos, lmin, lmax, ebase, nullptr, nullptr, nullptr, nullptr,
-                      nullptr, err, abl};
+                      nullptr, err, abl, walk_v};
     vbf::phase_begin(vbf::kPhaseSstWalk, s);
     HIP_TRY(vbf::sst_count(*a, s));
     vbf::phase_end(vbf::kPhaseSstWalk, s);

@@ -82,6 +82,7 @@ struct SstArgs {
     uint8_t* tomb;
     uint32_t* err;           // [0] error bits, [1] first bad block, [2]/[3] min/max key length
     uint32_t ablate;         // timing experiments only (VBF_ABLATE 11-14, ablation builds)
+    uint32_t walk_v;         // 1: vector-register entry walk (default), 0: scalar (VBF_SST_WALK)
 };
 hipError_t sst_count(const SstArgs& a, hipStream_t s);
 hipError_t sst_emit(const SstArgs& a, hipStream_t s);

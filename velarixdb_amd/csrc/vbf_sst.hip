@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <hipcub/device/device_reduce.hpp>
 #include <hipcub/device/device_scan.hpp>
 
@@ -162,6 +163,60 @@ __device__ __forceinline__ uint32_t walk_chain(const BlockView& v, uint32_t blen
     return n;
 }
 
+// The same walk with the chain in VECTOR registers (VBF_SST_WALK=1, default).  The scalar walk
+// spends ~20 SALU instructions per entry (readfirstlane'd state, m0, loop control), and a CU has
+// one scalar unit for all its waves, so the walk was SALU-bound.  Here the (uniform) state stays
+// in VGPRs: per entry an LDS read pair, v_alignbyte, a clamp-add and a masked select, and the
+// start lands in lane i of slot k by a compare/select.  Four entries per loop check; steps past
+// the block end leave p unchanged and record starts >= blen, which the count ignores.  Key length
+// range is reduced afterwards from the recorded starts, lane-parallel.  Same outputs and errors.
+template <bool LDS>
+__device__ __forceinline__ uint32_t walk_chain_v(const BlockView& v, uint32_t blen, uint32_t lane,
+                                                 uint32_t (&pr)[4], uint32_t& bad, uint32_t& lmin,
+                                                 uint32_t& lmax) {
+    // p starts in a VGPR the compiler must treat as divergent (an asm result), or its uniformity
+    // analysis would readfirstlane the LDS reads and put the chain back on the scalar unit.
+    uint32_t p;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(p));
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        pr[k] = 0xFFFFFFFFu;
+        if (p >= blen) continue;
+        for (uint32_t i = 0; i < 64; i += 4) {
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const bool has4 = p + 4 <= blen;  // a length field lies wholly inside the block
+                const uint32_t raw = v.u32(has4 ? p : 0u);  // always a safe read: no branch
+                const uint32_t L = has4 ? raw : 0x10000u;
+                pr[k] = lane == i + u ? p : pr[k];
+                const uint32_t pn = p + std::min(L, 0x10000u) + kEntryFixed;
+                p = p < blen ? pn : p;
+            }
+            if (p >= blen) break;
+        }
+    }
+    bad = p != blen ? (p < blen ? kSstErrDense : kSstErrCross) : 0;
+    uint32_t n = 0;
+    lmin = 0xFFFFFFFFu;
+    lmax = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const bool live = pr[k] < blen;
+        n += (uint32_t)__popcll(__ballot(live));
+        if (live) {
+            const uint32_t L = v.u32(pr[k]);
+            lmin = std::min(lmin, L);
+            lmax = std::max(lmax, L);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lmin = std::min(lmin, (uint32_t)__shfl_xor((int)lmin, o));
+        lmax = std::max(lmax, (uint32_t)__shfl_xor((int)lmax, o));
+    }
+    return n;
+}
+
 __global__ __launch_bounds__(64 * kSstWaves) void k_sst_walk(SstArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t stage[kSstWaves][kStage / 4 + 8];
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -192,8 +247,13 @@ __global__ __launch_bounds__(64 * kSstWaves) void k_sst_walk(SstArgs a) {
         }
         n = 124;
     } else {
-        n = v.lds ? walk_chain<true>(v, blen, lane, pr, bad, lmin, lmax)
-                  : walk_chain<false>(v, blen, lane, pr, bad, lmin, lmax);
+        static_assert(kMaxEnt == 256, "four 64-lane slots of entry starts");
+        if (a.walk_v)
+            n = v.lds ? walk_chain_v<true>(v, blen, lane, pr, bad, lmin, lmax)
+                      : walk_chain_v<false>(v, blen, lane, pr, bad, lmin, lmax);
+        else
+            n = v.lds ? walk_chain<true>(v, blen, lane, pr, bad, lmin, lmax)
+                      : walk_chain<false>(v, blen, lane, pr, bad, lmin, lmax);
     }
     if (bad) {
         if (lane == 0) sst_error(a, b, bad);
