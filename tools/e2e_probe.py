@@ -35,6 +35,9 @@ d = torch.empty(nb, dtype=torch.uint8, device=dev)
 print("H2D pinned   %.1f GB/s (%.1f ms)" % rate(lambda: d.copy_(pin, non_blocking=True), nb))
 print("H2D pageable %.1f GB/s (%.1f ms)" % rate(lambda: d.copy_(pag), nb))
 print("D2H pinned   %.1f GB/s (%.1f ms)" % rate(lambda: pin.copy_(d, non_blocking=True), nb))
+print("D2H pageable %.1f GB/s (%.1f ms)" % rate(lambda: pag.copy_(d), nb))
+fresh = lambda: torch.empty(125_000_000, dtype=torch.uint8).copy_(d[:125_000_000])
+print("D2H 125 MB into a fresh pageable tensor %.1f GB/s (%.1f ms)" % rate(fresh, 125_000_000))
 a = np.ones(nb, np.uint8)
 b = np.empty(nb, np.uint8)
 t0 = time.perf_counter()
@@ -54,3 +57,20 @@ for rep in range(3):
     vbf._lib.call("vbf_build_host", host.ctypes.data, None, L, n, 1, m, k, words.ctypes.data, words.size, 0)
     print("vbf_build_host 100M x 16 B (VBF_COPY_THREADS=%s): %.1f ms"
           % (os.environ.get("VBF_COPY_THREADS", "default"), (time.perf_counter() - t0) * 1e3))
+
+# phases of bench.py --e2e's step (BloomFilter::new -> set over host keys -> words to host)
+from velarixdb_amd.keys import HostBatch  # noqa: E402
+hb = HostBatch(host, None, L, n, 1)
+p = wl.fpr_for_bits_per_key(10)
+for rep in range(4):
+    t0 = time.perf_counter()
+    bf = vbf.BloomFilter(p, n, device=0)
+    t1 = time.perf_counter()
+    bf.set_batch(hb)
+    t2 = time.perf_counter()
+    w = bf.words()
+    t3 = time.perf_counter()
+    del bf
+    t4 = time.perf_counter()
+    print("e2e phases: new %.2f  set_batch %.2f  words %.2f  free %.2f ms" % ((t1 - t0) * 1e3, (t2 - t1) * 1e3,
+                                                                          (t3 - t2) * 1e3, (t4 - t3) * 1e3))

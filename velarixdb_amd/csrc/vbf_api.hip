@@ -325,8 +325,13 @@ int xfer_bufs(Staging& st) {
     return VBF_OK;
 }
 
+bool d2h_direct() {  // VBF_D2H_DIRECT=1: pageable hipMemcpy instead of the bounce (A/B)
+    static const bool v = [] { const char* e = getenv("VBF_D2H_DIRECT"); return e && atoi(e) != 0; }();
+    return v;
+}
+
 int xfer_d2h(Staging& st, void* dst, const void* src, uint64_t bytes) {
-    if (bytes < kXferDirect) {
+    if (bytes < kXferDirect || d2h_direct()) {
         HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
         return VBF_OK;
     }
