@@ -36,7 +36,7 @@ def _worker(rank, world, port, m, k, n, q):
         nwords = (m + 31) // 32
         buf, chunk = padded_words(nwords, world, "cpu")
         buf[:nwords] = torch.from_numpy(partial.view(np.int32))
-        or_allreduce_(buf, chunk)
+        or_allreduce_(buf, chunk, or_into=lambda a, b: a.bitwise_or_(b))  # gloo: CPU tensors
         q.put((rank, buf[:nwords].numpy().view(np.uint32).copy(), buf[nwords:].abs().sum().item()))
     finally:
         dist.destroy_process_group()

@@ -24,14 +24,12 @@ def shard_range(n, rank, world):
     return lo, hi
 
 
-def _or_into(acc, src):
-    """acc |= src, same shape int32 tensors."""
-    if acc.device.type == "cuda":
-        stream = ctypes.c_void_p(torch.cuda.current_stream(acc.device).cuda_stream)
-        call("vbf_or_words_dev", ctypes.c_void_p(acc.data_ptr()), ctypes.c_void_p(src.data_ptr()),
-             acc.numel(), stream)
-    else:  # gloo (CPU) process groups: the world_size>1 tests of this exchange
-        acc.bitwise_or_(src)
+def or_words_dev(acc, src):
+    """acc |= src on the GPU (HIP kernel vbf_or_words_dev); same-shape int32 device tensors."""
+    if acc.device.type != "cuda" or src.device.type != "cuda":
+        raise ValueError("or_words_dev needs device tensors (the OR runs as a HIP kernel)")
+    stream = ctypes.c_void_p(torch.cuda.current_stream(acc.device).cuda_stream)
+    call("vbf_or_words_dev", ctypes.c_void_p(acc.data_ptr()), ctypes.c_void_p(src.data_ptr()), acc.numel(), stream)
 
 
 def padded_words(nwords, world, device):
@@ -41,8 +39,9 @@ def padded_words(nwords, world, device):
     return torch.zeros(chunk * world, dtype=torch.int32, device=device), chunk
 
 
-def or_allreduce_(buf, chunk, group=None):
-    """In place: buf (padded_words layout) becomes the OR of every rank's buf."""
+def or_allreduce_(buf, chunk, group=None, or_into=or_words_dev):
+    """In place: buf (padded_words layout) becomes the OR of every rank's buf.  The local OR is
+    the HIP kernel; the CPU (gloo) tests of the exchange pattern pass their own `or_into`."""
     if not dist.is_initialized():
         return buf
     world = dist.get_world_size(group)
@@ -52,6 +51,6 @@ def or_allreduce_(buf, chunk, group=None):
     dist.all_to_all_single(recv, buf, group=group)
     acc = recv[:chunk].clone()
     for r in range(1, world):
-        _or_into(acc, recv[r * chunk:(r + 1) * chunk])
+        or_into(acc, recv[r * chunk:(r + 1) * chunk])
     dist.all_gather_into_tensor(buf, acc, group=group)
     return buf
