@@ -422,3 +422,23 @@ def test_concentrated_indices(vbf, ora, strategy):
         assert int(cnt.item()) == b.n, ps
     neg = pack_fixed(rng.integers(0, 256, (200_000, 16), dtype=np.uint8))
     assert not gpu_probe(vbf, neg, m, k, got).any()  # 40 bits of 1e9: no false positive expected
+
+
+def test_or_words_kernel(vbf):
+    """vbf_or_words_dev (the local OR of the multi-GPU filter merge, dist.or_words_dev): equal to
+    a bitwise OR for ragged lengths; misaligned pointers are refused."""
+    from velarixdb_amd.dist import or_words_dev
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    for n in (1, 3, 4, 1023, 1 << 20, (1 << 20) + 5):
+        a = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
+        b = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device=DEV, generator=g)
+        want = a | b
+        or_words_dev(a, b)
+        torch.cuda.synchronize()
+        assert torch.equal(a, want), n
+    a = torch.zeros(9, dtype=torch.int32, device=DEV)
+    with pytest.raises(vbf.VbfError):
+        vbf._lib.call("vbf_or_words_dev", _ptr(a[1:]), _ptr(a[:8]), 8, _stream())
+    with pytest.raises(ValueError):
+        or_words_dev(torch.zeros(4, dtype=torch.int32), torch.zeros(4, dtype=torch.int32))
