@@ -157,10 +157,11 @@ def test_config1_bit_exact(vbf, ora):
 
 
 @pytest.mark.parametrize("strategy", [ATOMIC, PARTITIONED])
-def test_build_variable_length_matches_oracle(vbf, ora, strategy):
+@pytest.mark.parametrize("k", [10, 7, 19])  # compile-time K (10, 19) and the runtime-k kernel (7)
+def test_build_variable_length_matches_oracle(vbf, ora, strategy, k):
     from velarixdb_amd.keys import pack_offsets
     from velarixdb_amd.workloads import SEED_CFG3, SEED_CFG3_NEG, var_offsets
-    n, m, k = 100_000, 1_000_003, 10
+    n, m = 100_000, 1_000_003
     off = var_offsets(SEED_CFG3, 0, n)
     data = ora.gen_var(SEED_CFG3, 0, off)
     b = pack_offsets(data, off)
