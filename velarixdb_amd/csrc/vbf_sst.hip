@@ -203,7 +203,7 @@ __device__ __forceinline__ uint32_t walk_chain_v(const BlockView& v, uint32_t bl
     for (uint32_t k = 0; k < 4; ++k) {
         const bool live = pr[k] < blen;
         n += (uint32_t)__popcll(__ballot(live));
-        if (live) {
+        if (live && pr[k] + 4 <= blen) {  // a malformed tail start is reported, never read past blen
             const uint32_t L = v.u32(pr[k]);
             lmin = std::min(lmin, L);
             lmax = std::max(lmax, L);
