@@ -85,6 +85,8 @@ def test_fixture_rebuild_matches_golden(vbf, golden, tmp_path):
     (6, 20000, [0]),                       # empty keys only: 240 entries per 4080-byte block
     (7, 20000, [16]),
     (8, 4000, [1, 2, 3, 5, 8, 13, 21, 34, 55, 89, 144, 233, 377, 610, 987]),
+    (9, 20000, [16] * 60 + [17]),          # near-uniform: most blocks fail the fixed-size guess late
+    (10, 20000, [16] * 200 + [0]),
 ])
 def test_random_sst_decode(vbf, ora, seed, n, lengths):
     data, index, ref = _rand_sst(ora, seed, n, lengths)
@@ -219,3 +221,19 @@ def test_large_sst_decode_properties(vbf):
     ref.set_dev(P(keys), None, L, n, 1, sp)
     torch.cuda.synchronize()
     assert np.array_equal(bf.words(), ref.words())
+
+
+def test_uniform_guess_cannot_be_fooled(vbf, ora):
+    """The walk's fixed-size fast path (entry i at i * (L0 + 17)) is verified at every predicted
+    start.  Keys whose bytes spell LE32(16) everywhere, with lengths 16 and 20 mixed, put the
+    first entry's length at many wrong offsets; the decode must still follow the real chain."""
+    rng = np.random.default_rng(12)
+    n = 30000
+    L = rng.choice(np.array([16, 16, 16, 20], np.uint64), size=n)
+    offs = np.concatenate([[0], np.cumsum(L)]).astype(np.uint64)
+    keys = np.tile(np.frombuffer(np.uint32(16).tobytes(), np.uint8), int(offs[-1]) // 4 + 1)[: int(offs[-1])].copy()
+    val = np.full(n, 16, np.uint32)
+    created = np.full(n, 16, np.uint64)
+    tomb = np.zeros(n, np.uint8)
+    data, index = ora.sst_write(keys, offs, val, created, tomb)
+    _same(vbf.sst.load_entries(data, index), (keys, offs, val, created, tomb))

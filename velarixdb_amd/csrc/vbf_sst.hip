@@ -217,6 +217,34 @@ __device__ __forceinline__ uint32_t walk_chain_v(const BlockView& v, uint32_t bl
     return n;
 }
 
+// Fixed-size entries (every key of the block as long as the first one -- the common case for
+// SSTables of fixed-width keys): entry i then starts at i * (L0 + 17).  The guess is checked
+// lane-parallel -- the block length is a whole number of such entries and every predicted
+// start holds L0 -- and when it holds, the chain walk from 0 would visit exactly these starts
+// and end at blen, so the result is identical without the 100+-step dependent chain.  Any
+// mismatch (mixed lengths, malformed blocks) falls back to the walk, which reports errors.
+template <class View>
+__device__ __forceinline__ bool uniform_block(const View& v, uint32_t blen, uint32_t lane, uint32_t (&pr)[4],
+                                              uint32_t& n, uint32_t& lmin, uint32_t& lmax) {
+    if (blen < 4) return false;
+    const uint32_t L0 = v.u32(0);
+    if (L0 > 0xFFFFu) return false;
+    const uint32_t E = L0 + kEntryFixed;
+    if (blen % E != 0 || blen / E > kMaxEnt) return false;
+    const uint32_t cnt = blen / E;
+    bool ok = true;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t i = lane + 64 * k;
+        pr[k] = i < cnt ? i * E : 0xFFFFFFFFu;
+        if (i < cnt) ok &= v.u32(i * E) == L0;
+    }
+    if (__ballot(!ok)) return false;
+    n = cnt;
+    lmin = lmax = L0;
+    return true;
+}
+
 __global__ __launch_bounds__(64 * kSstWaves) void k_sst_walk(SstArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t stage[kSstWaves][kStage / 4 + 8];
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -248,7 +276,9 @@ __global__ __launch_bounds__(64 * kSstWaves) void k_sst_walk(SstArgs a) {
         n = 124;
     } else {
         static_assert(kMaxEnt == 256, "four 64-lane slots of entry starts");
-        if (a.walk_v)
+        if (a.walk_v && uniform_block(v, blen, lane, pr, n, lmin, lmax)) {
+            // every entry has the first entry's key length: starts known without the chain
+        } else if (a.walk_v)
             n = v.lds ? walk_chain_v<true>(v, blen, lane, pr, bad, lmin, lmax)
                       : walk_chain_v<false>(v, blen, lane, pr, bad, lmin, lmax);
         else
