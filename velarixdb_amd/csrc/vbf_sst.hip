@@ -289,10 +289,14 @@ __global__ __launch_bounds__(64 * kSstWaves) void k_sst_walk(SstArgs a) {
         if (lane == 0) sst_error(a, b, bad);
         return;
     }
+    // Blocks whose keys all have one length need no starts: entry i is at i * (L + 17), which
+    // is how the emit pass finds them (lmin == lmax), so the 512-byte start list is not written.
     uint16_t* out = a.pos + b * kMaxEnt;
+    if (lmin != lmax) {
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-        if (lane + 64 * k < n) out[lane + 64 * k] = (uint16_t)pr[k];
+        for (uint32_t k = 0; k < 4; ++k)
+            if (lane + 64 * k < n) out[lane + 64 * k] = (uint16_t)pr[k];
+    }
     if (lane == 0) {
         a.counts[b] = n;
         a.lmin[b] = lmin;  // key-length range (reduced after the pass): uniform lengths let the
@@ -310,14 +314,19 @@ __global__ __launch_bounds__(64 * kSstWaves) void k_sst_emit(SstArgs a) {
     const uint64_t s = a.blocks[b];
     const uint32_t blen = (uint32_t)((b + 1 < a.nblocks ? a.blocks[b + 1] : a.len) - s);  // validated by pass 1
     const uint32_t n = a.counts[b];
+    const uint32_t L0 = a.lmin[b];
+    const bool uni = a.lmax[b] == L0;  // one key length: entry i starts at i * (L0 + 17)
     uint16_t* ps = pos[wave];
-    const uint16_t* pin = a.pos + b * kMaxEnt;
-    for (uint32_t i = lane; i < n; i += 64) ps[i] = pin[i];
+    if (!uni) {
+        const uint16_t* pin = a.pos + b * kMaxEnt;
+        for (uint32_t i = lane; i < n; i += 64) ps[i] = pin[i];
+    }
     const BlockView v = stage_block(a, s, blen, stage[wave], lane);  // its barrier covers ps too
+    auto start = [&](uint32_t i) { return uni ? i * (L0 + kEntryFixed) : (uint32_t)ps[i]; };
     const uint64_t E = a.ebase[b];
     const uint64_t G = s - (uint64_t)kEntryFixed * E;  // key bytes before this block
     for (uint32_t i = lane; i < n; i += 64) {
-        const uint32_t q = ps[i];
+        const uint32_t q = start(i);
         const uint32_t L = v.u32(q);
         if (a.offsets) a.offsets[E + i] = G + q - kEntryFixed * i;
         if (a.val_off) a.val_off[E + i] = v.u32(q + 4 + L);
@@ -327,9 +336,20 @@ __global__ __launch_bounds__(64 * kSstWaves) void k_sst_emit(SstArgs a) {
     const uint64_t K = blen - (uint64_t)kEntryFixed * n;  // this block's key bytes
     if (a.offsets && b + 1 == a.nblocks && lane == 0) a.offsets[E + n] = G + K;
     if (!a.keys || K == 0) return;
+    // Fixed-size entries whose key length is a multiple of 4 (the walk's fast-path layout, with
+    // G then dword aligned): output dword x is word x % (L0/4) of key x / (L0/4) -- no search.
+    if (uni && (L0 & 3) == 0 && (G & 3) == 0) {
+        const uint32_t wpk = L0 >> 2, nw = (uint32_t)(K >> 2);
+        uint32_t* kout = reinterpret_cast<uint32_t*>(a.keys + G);
+        for (uint32_t x = lane; x < nw; x += 64) {
+            const uint32_t i = x / wpk;
+            kout[x] = v.u32(4 * x + 4 + kEntryFixed * i);
+        }
+        return;
+    }
     // packed key bytes [G, G + K), one lane per aligned output dword: output byte d lies in the
     // last entry i with cum(i) = pos(i) - 17 i <= d, at block byte d + 4 + 17 i
-    auto cum = [&](uint32_t i) { return (uint32_t)ps[i] - kEntryFixed * i; };
+    auto cum = [&](uint32_t i) { return start(i) - kEntryFixed * i; };
     const uint64_t w_lo = G >> 2, w_hi = (G + K + 3) >> 2;
     uint32_t hint = 0;  // lanes move forward through the block: start the search at the last hit
     for (uint64_t w = w_lo + lane; w < w_hi; w += 64) {
