@@ -125,11 +125,12 @@ def test_config5_sizing_slice(vbf, ora):
 
 
 def test_multi_chunk_partitioned_paths(vbf):
-    """More than kPartChunkIdx (2^30) bit indices in one call: the partitioned build and the
-    partitioned probe process the batch in chunks.  The chunked build must equal the per-key
-    atomic build bit for bit, and both probe strategies must find every key."""
+    """More bit indices in one call than one chunk holds (build: kBuildChunkIdx = 2^31, probe:
+    kPartChunkIdx = 2^30): both partitioned paths process the batch in chunks.  The chunked
+    build must equal the per-key atomic build bit for bit, and both probe strategies must find
+    every key."""
     from velarixdb_amd.workloads import SEED_CFG2
-    n, L, m, k = 120_000_000, 16, 1_200_000_000, 10  # 1.2e9 indices -> two chunks
+    n, L, m, k = 220_000_000, 16, 2_200_000_000, 10  # 2.2e9 indices: 2 build / 3 probe chunks
     keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
     vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG2 ^ 0x77, 0, n, L, vp(keys), sp())
     w_part = build(vbf, keys, None, L, n, m, k, 2)

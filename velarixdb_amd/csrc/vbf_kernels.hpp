@@ -35,8 +35,11 @@ void phase_begin(int phase, hipStream_t s);
 void phase_end(int phase, hipStream_t s);
 
 // Partitioned build (vbf_partition.hip).  Key batches are processed in chunks of at most
-// kPartChunkIdx bit indices; the workspace holds one chunk's sorted tiles + offset tables.
+// kBuildChunkIdx (build) / kPartChunkIdx (probe) bit indices; the workspace holds one chunk's
+// sorted tiles + offset tables (build: 2.5 B per index, ~5.4 GB at 2^31; probe: 4 B per index).
+// Each build chunk re-reads and re-writes the whole filter in k_seg_or, so build chunks are big.
 constexpr uint64_t kPartChunkIdx = 1ull << 30;
+constexpr uint64_t kBuildChunkIdx = 1ull << 31;
 bool partition_supported(uint32_t m, uint32_t k);
 uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
 // Partitioned probe (vbf_partition.hip): out (answer bytes) or count (hits), one of them.

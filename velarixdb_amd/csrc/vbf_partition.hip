@@ -45,10 +45,15 @@ constexpr uint32_t kNibMask = (1u << (kSegBits - 16)) - 1;  // in-segment offset
 static_assert(kSegBits > 16 && kSegBits <= 20, "offset = u16 + up to 4 nibble bits");
 constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a bit index: idx < m <= 2^32 - 1
 constexpr uint32_t kLdsPerCu = 163840;
+constexpr uint32_t kShortRun = 24;  // mean entries per (tile, segment) run below which K3 flattens
 
 // Rounds of 1024 keys a lane can stash: kStash / k indices, but k = 4 keeps 24 so the fully
 // unrolled K = 4 kernel stays within 64 VGPRs (two workgroups per CU) without spilling.
 __host__ __device__ constexpr int rounds_max(int k) { return k == 4 ? 6 : kStash / k; }
+// Stash rounds of the build kernels.  (Two rounds for K = 19, velarixdb's default p = 1e-4,
+// would fill the tile's LDS image -- ~1 600 keys instead of 1 024 -- but 38 stashed indices
+// spill past the 64 VGPRs that two workgroups per CU allow; measured, not kept.)
+__host__ __device__ constexpr int build_rounds_max(int k) { return rounds_max(k); }
 
 struct PartPlan {
     uint32_t k;
@@ -61,7 +66,7 @@ struct PartPlan {
     uint32_t lds1;        // K1 dynamic LDS bytes
     uint32_t stagger_lo, stagger_hi, stagger_sleeps;
     uint32_t ablate;      // ablation builds only (VBF_ABLATE, vbf_kernels.hpp): 1 skip place+copy
-    uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or)
+    uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or); 0 = by run length
     uint64_t m, mu, nwords;
 };
 
@@ -158,7 +163,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     if (FMT < 0 && tid < kLenBuckets) lhist[tid] = 0;
     __syncthreads();
 
-    uint32_t stash[kStash];
+    uint32_t stash[K > 0 ? build_rounds_max(K) * K : kStash];
     const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
     const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
     const uint32_t nk = (uint32_t)(key_end - key0);
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     auto key_of = [&](uint32_t slot) -> uint64_t { return key0 + (FMT < 0 ? (uint32_t)lo[slot] : slot); };
     uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     if constexpr (K > 0) {
-        constexpr int RM = rounds_max(K);
+        constexpr int RM = build_rounds_max(K);
 #pragma unroll
         for (int r = 0; r < RM; ++r) {
             const uint32_t slot = (uint32_t)r * kPBlock + tid;
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     }
     // rank + place, 8 returning LDS atomics in flight before their results are used
     // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
-    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(rounds_max(K) * K) : (uint32_t)kStash;
+    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(build_rounds_max(K) * K) : (uint32_t)kStash;
 #pragma unroll
     for (uint32_t t = 0; t < kNsMax; t += 8) {
         if (t >= ns) break;
@@ -305,19 +310,20 @@ __device__ __forceinline__ void load8(const uint32_t* tile, uint32_t cp, uint32_
     nib = (uint32_t)(hh >> ((e & 7) * 4));
 }
 
-// K3 tile-loop variants (VBF_K3, speed only; identical results):
-//   0: two-stage -- run bounds of batch b+1 (8 u16 loads per lane) in flight with batch b's data
+// K3 tile-loop variants (speed only; identical results).  By default the plan picks V3 (NG = 5)
+// for runs of >= kShortRun entries on average (C / nseg) and V6 (NG = 4) below; VBF_K3 forces one:
+//   1: two-stage -- run bounds of batch b+1 (8 u16 loads per lane) in flight with batch b's data
 //   3: three-stage -- bounds of b+2, data of b+1 and the ORs of b overlap; run bounds loaded
 //      coalesced (one u16 pair per lane for the wave's tiles) and handed to the 8-lane groups with
 //      ds_bpermute; data loads unconditional (idle lanes re-read their run's first 8 entries) so
 //      vmcnt waits stay exact; NG runs per 8-lane group per batch (VBF_K3 3: 1024 threads NG=4;
-//      4 (default): 1024, NG=5; 5: 768, NG=6; 6: 768, NG=8).
+//      4: 1024, NG=5; 5: 768, NG=6; 6: 768, NG=8).
+//   6: flattened chunks in the three-stage pipeline -- no lane idles on a short run (VBF_K3 10:
+//      NG=4, 11: NG=5).  0.95 vs 1.03 ms at k = 10 (31-entry runs), but at k = 19 (m = 1.9e9,
+//      ~11-entry runs) it is the one that keeps K3 from idling 5/6 of its lanes.
 //   Measured and dropped (tools/env_ab.sh): coalesced bounds in the two-stage loop (-3 %);
 //   raw buffer loads with out-of-range offsets for idle lanes (no duplicate requests): 0.92 ms,
-//   the same as the duplicates (the texture addresser coalesces them);
-//   "flattened" chunks -- a wave's runs cut into 8-entry chunks dealt to lanes back to back,
-//   found by binary search over the chunk prefix, so no lane idles -- 1.03-1.05 ms alone or
-//   three-stage, vs 0.95 ms: the idle lanes' duplicate loads are not what bounds the kernel.
+//   the same as the duplicates (the texture addresser coalesces them).
 template <int V, int BS = kPBlock, int NG = 8>
 __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint16_t* endsT,
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
@@ -377,6 +383,90 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
 
     if (pl.ablate >= 5) {
         // 5-7: timing experiments, fixed costs only
+    } else if constexpr (V == 6) {
+        // Flattened chunks for SHORT runs (large k or m: C / nseg entries per run): a wave's 64
+        // runs (one per tile, bounds in lane order) are cut into 8-entry chunks dealt to lanes
+        // back to back, so no lane idles on a short run.  A lane finds its run by a 6-step binary
+        // search over the wave's exclusive chunk prefix (ds_bpermute).  Pipelined like V3: the
+        // bounds of batch b+2, the chunk loads of batch b+1 and the ORs of batch b in flight
+        // together.  Chunks beyond NG * 64 per batch are loaded and ORed at consume time.
+        const uint32_t wstep = (BS / 64) * 64;
+        struct FB {
+            uint32_t v, excl, total;
+            uint4 l[NG];
+            uint32_t nib[NG], cnt[NG];
+        };
+        auto prep = [&](uint32_t v, FB& b) {
+            const uint32_t ch = (((v >> 16) - (v & 0xFFFFu)) + 7) >> 3;
+            uint32_t incl = ch;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= (uint32_t)o) incl += y;
+            }
+            b.v = v;
+            b.excl = incl - ch;
+            b.total = (uint32_t)__shfl((int)incl, 63);
+        };
+        // chunk c of the batch at t0 -> (tile, entry offset, live entries)
+        auto locate = [&](const FB& b, uint32_t t0, uint32_t c, const uint32_t*& tile, uint32_t& e) -> uint32_t {
+            uint32_t r = 0;
+#pragma unroll
+            for (int sft = 32; sft; sft >>= 1)
+                if ((uint32_t)__shfl((int)b.excl, (int)r + sft) <= c) r += sft;
+            const uint32_t rv = (uint32_t)__shfl((int)b.v, (int)r), rex = (uint32_t)__shfl((int)b.excl, (int)r);
+            const uint32_t rst = rv & 0xFFFFu, rlen = (rv >> 16) - rst, off = (c - rex) * 8;
+            tile = tiles + (uint64_t)std::min(t0 + r, t_hi - 1) * pl.tile_words;
+            e = rst + off;
+            return c < b.total ? std::min<uint32_t>(8, rlen - off) : 0u;
+        };
+        auto issue = [&](uint32_t t0, FB& b) {
+#pragma unroll
+            for (int q = 0; q < NG; ++q) {
+                const uint32_t* tile;
+                uint32_t e;
+                b.cnt[q] = locate(b, t0, (uint32_t)q * 64 + lane, tile, e);
+                if (b.cnt[q]) load8(tile, pl.CP, e, b.l[q], b.nib[q]);
+            }
+        };
+        auto consume = [&](uint32_t t0, const FB& b) {
+#pragma unroll
+            for (int q = 0; q < NG; ++q)
+                if (b.cnt[q]) or8(bitmap, b.l[q], b.nib[q], b.cnt[q]);
+#pragma unroll 1
+            for (uint32_t c0 = 64 * NG; c0 < b.total; c0 += 64) {
+                const uint32_t* tile;
+                uint32_t e;
+                const uint32_t n8 = locate(b, t0, c0 + lane, tile, e);
+                if (n8) {
+                    uint4 lt;
+                    uint32_t nt;
+                    load8(tile, pl.CP, e, lt, nt);
+                    or8(bitmap, lt, nt, n8);
+                }
+            }
+        };
+        uint32_t t0 = t_lo + wave * 64;
+        FB A, B;
+        uint32_t v1 = lb(t0 + wstep);
+        prep(lb(t0), A);
+        if (t0 < t_hi) issue(t0, A);
+        while (t0 < t_hi) {
+            prep(v1, B);
+            uint32_t v2 = lb(t0 + 2 * wstep);
+            const bool more = t0 + wstep < t_hi;
+            if (more) issue(t0 + wstep, B);
+            consume(t0, A);
+            t0 += wstep;
+            if (!more) break;
+            prep(v2, A);
+            v1 = lb(t0 + 2 * wstep);
+            const bool more2 = t0 + wstep < t_hi;
+            if (more2) issue(t0 + wstep, A);
+            consume(t0, B);
+            t0 += wstep;
+            if (!more2) break;
+        }
     } else if constexpr (V == 3) {
         struct Batch {
             uint32_t be[NG];
@@ -509,7 +599,9 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.nwords = ((uint64_t)m + 31) / 32;
     pl.nseg = (uint32_t)(((uint64_t)m + (1u << kSegBits) - 1) >> kSegBits);
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
-    const uint32_t rmax = (uint32_t)rounds_max((int)k);
+    // runtime k (the K = 0 kernel) keeps kStash / k rounds; compiled K values their own
+    const bool ck = k == 4 || k == 9 || k == 10 || k == 19;
+    const uint32_t rmax = (uint32_t)(ck ? build_rounds_max((int)k) : rounds_max((int)k));
     for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
         const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)pl.nseg_pad;
@@ -538,7 +630,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
         return e ? atoi(e) : 0;
     }();
     pl.ablate = (uint32_t)abl;
-    static const int k3v = [] { const char* e = getenv("VBF_K3"); return e ? atoi(e) : 4; }();
+    static const int k3v = [] { const char* e = getenv("VBF_K3"); return e ? atoi(e) : 0; }();
     pl.k3v = (uint32_t)k3v;
     return pl;
 }
@@ -550,7 +642,7 @@ bool partition_supported(uint32_t m, uint32_t k) {
 }
 
 static uint64_t chunk_keys_for(const PartPlan& pl, uint64_t n) {
-    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, kPartChunkIdx / pl.C);
+    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, kBuildChunkIdx / pl.C);
     return std::min<uint64_t>(n, tiles_per_chunk * pl.KT);
 }
 
@@ -605,12 +697,16 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         const bool merge = atomic_merge || pl.G > 1;
         phase_end(kPhaseTranspose, s);
         phase_begin(kPhaseSegOr, s);
-        auto k3 = pl.k3v == 3 ? k_seg_or<3, kPBlock, 4>
-                : pl.k3v == 4 ? k_seg_or<3, kPBlock, 5>
-                : pl.k3v == 5 ? k_seg_or<3, 768, 6>
-                : pl.k3v == 6 ? k_seg_or<3, 768, 8>
-                              : k_seg_or<0>;
-        const int bs = (pl.k3v == 5 || pl.k3v == 6) ? 768 : kPBlock;
+        // short runs (large k or m): the flattened variant; VBF_K3 overrides
+        const uint32_t k3v = pl.k3v ? pl.k3v : (pl.C / std::max(pl.nseg, 1u) < kShortRun ? 10u : 4u);
+        auto k3 = k3v == 10 ? k_seg_or<6, kPBlock, 4>
+                : k3v == 11 ? k_seg_or<6, kPBlock, 5>
+                : k3v == 3 ? k_seg_or<3, kPBlock, 4>
+                : k3v == 5 ? k_seg_or<3, 768, 6>
+                : k3v == 6 ? k_seg_or<3, 768, 8>
+                : k3v == 1 ? k_seg_or<0>
+                           : k_seg_or<3, kPBlock, 5>;
+        const int bs = (k3v == 5 || k3v == 6) ? 768 : kPBlock;
         hipLaunchKernelGGL(k3, dim3(pl.nseg * pl.G), dim3(bs), 0, s, tiles, endsT, ntiles, pl, merge, words);
         phase_end(kPhaseSegOr, s);
         err = hipGetLastError();
