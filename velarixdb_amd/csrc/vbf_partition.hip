@@ -1071,6 +1071,7 @@ hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
             auto fn = k == 10 ? k_probe_pack<FMT, LP, 10>
                     : k == 4  ? k_probe_pack<FMT, LP, 4>
+                    : k == 19 ? k_probe_pack<FMT, LP, 19>  // the reference's default p = 1e-4
                               : k_probe_pack<FMT, LP, 0>;
             err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
