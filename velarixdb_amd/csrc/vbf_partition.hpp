@@ -1,0 +1,80 @@
+// vbf_partition.hpp -- constants and LDS helpers shared by the partitioned build
+// (vbf_partition.hip) and the partitioned probe (vbf_probe_part.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstdlib>
+
+#include "keyhash.hpp"
+#include "sip13.hpp"
+#include "vbf_kernels.hpp"
+
+#ifndef VBF_SEG_BITS
+#define VBF_SEG_BITS 20
+#endif
+
+namespace vbf {
+
+constexpr int kPBlock = 1024;                // threads per K1 / K3 workgroup
+constexpr int kStash = 32;                   // max bit indices a lane keeps in registers
+constexpr int kSegBits = VBF_SEG_BITS;       // segment = 2^20 bits = 128 KiB of LDS (default)
+constexpr uint32_t kSegWords = 1u << (kSegBits - 5);
+constexpr uint32_t kNibMask = (1u << (kSegBits - 16)) - 1;  // in-segment offset bits above 16
+static_assert(kSegBits > 16 && kSegBits <= 20, "offset = u16 + up to 4 nibble bits");
+constexpr uint32_t kSentinel = 0xFFFFFFFFu;  // never a bit index: idx < m <= 2^32 - 1
+constexpr uint32_t kLdsPerCu = 163840;
+constexpr uint32_t kShortRun = 24;  // mean entries per (tile, segment) run below which K3 flattens
+
+// Rounds of 1024 keys a lane can stash: kStash / k indices, but k = 4 keeps 24 so the fully
+// unrolled K = 4 kernel stays within 64 VGPRs (two workgroups per CU) without spilling.
+__host__ __device__ constexpr int rounds_max(int k) { return k == 4 ? 6 : kStash / k; }
+// Stash rounds of the build kernels.  (Two rounds for K = 19, velarixdb's default p = 1e-4,
+// would fill the tile's LDS image -- ~1 600 keys instead of 1 024 -- but 38 stashed indices
+// spill past the 64 VGPRs that two workgroups per CU allow; measured, not kept.)
+__host__ __device__ constexpr int build_rounds_max(int k) { return rounds_max(k); }
+
+// Exclusive scan of v[0..n) in LDS (n <= 4 * kPBlock).
+__device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, uint32_t* wsum) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t loc[4];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t s = tid * 4 + q;
+        loc[q] = s < n ? v[s] : 0;
+        sum += loc[q];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    if (wave == 0) {
+        const uint32_t w = lane < kPBlock / 64 ? wsum[lane] : 0;
+        uint32_t wi = w;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t y = __shfl_up(wi, o);
+            if (lane >= (uint32_t)o) wi += y;
+        }
+        if (lane < kPBlock / 64) wsum[lane] = wi - w;
+    }
+    __syncthreads();
+    uint32_t run = wsum[wave] + incl - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t s = tid * 4 + q;
+        if (s < n) v[s] = run;
+        run += loc[q];
+    }
+}
+
+// K2 (vbf_partition.hip): ends[rows][cols] -> endsT[cols][rows], shared by build and probe.
+void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t s);
+
+}  // namespace vbf

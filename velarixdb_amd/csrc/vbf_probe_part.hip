@@ -1,0 +1,400 @@
+// vbf_probe_part.hip -- the partitioned probe (contains() for large batches): the build's
+// tile/segment scheme (vbf_partition.hip) applied to lookups.
+#include "vbf_partition.hpp"
+
+namespace vbf {
+
+// =================================================================================================
+// Partitioned probe (contains() for large batches, bf.rs:95-105).  The same idea as the build:
+// random filter loads (~55 G/s chip-wide) become LDS bit tests.
+//   Q1 k_probe_pack : per tile of keys, hash all k indices, sort the entries (tile-local key id
+//                     << 20 | offset in segment) by 2^20-bit segment in LDS, write each run padded
+//                     to a multiple of 8 entries (repeating its last entry) + the padded run ends.
+//   (K2 transpose of the run ends, shared with the build)
+//   Q3 k_probe_seg  : one workgroup per segment loads the segment's 128 KiB of filter words into
+//                     LDS once and tests every tile's run against it, 8 entries -> 1 result byte.
+//   Q4 k_probe_out  : per tile, AND each key's k results (a clear bit anywhere -> false) and write
+//                     the answer byte (or count the hits).
+// Without early exit every key costs k hashes, but no probe leaves the chip's LDS.
+// =================================================================================================
+struct ProbePlan {
+    uint32_t k, R, KT, C, nseg, nseg_pad, cap, lds1;
+    uint64_t m, mu, nwords;
+};
+
+constexpr uint32_t kOffMask = (1u << kSegBits) - 1;
+static_assert(kSegBits == 20, "probe entries hold a 12-bit key id above the 20-bit offset");
+
+template <int FMT, bool LP, int K, bool M31>
+__global__ __launch_bounds__(kPBlock) void k_probe_pack(DevKeys dk, ProbePlan pl, uint32_t* tiles, uint16_t* ends) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t* ent = smem;               // C entries
+    uint32_t* cnt = ent + pl.C;         // nseg_pad: counts -> starts -> ends
+    uint32_t* pst = cnt + pl.nseg_pad;  // nseg_pad: padded starts
+    uint32_t* wsum = pst + pl.nseg_pad; // 16
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
+    __syncthreads();
+    uint32_t stash[kStash];
+    const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
+    const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
+    uint32_t ns;
+    if constexpr (K > 0) {
+        constexpr int RM = rounds_max(K);
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+            const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
+            const bool valid = (uint32_t)r < pl.R && j < key_end;
+            Prefix p{};
+            if (valid) p = key_prefix<FMT, LP>(dk, j);
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                uint32_t idx = kSentinel;
+                if (valid) {
+                    idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
+                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                }
+                stash[r * K + i] = idx;
+            }
+        }
+        ns = RM * K;
+    } else {
+        ns = 0;
+        for (uint32_t r = 0; r < pl.R; ++r) {
+            const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
+            const bool valid = j < key_end;
+            Prefix p{};
+            if (valid) p = key_prefix<FMT, LP>(dk, j);
+            for (uint32_t i = 0; i < pl.k; ++i) {
+                uint32_t idx = kSentinel;
+                if (valid) {
+                    idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
+                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                }
+                stash[ns++] = idx;
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) pst[s] = (cnt[s] + 7) & ~7u;
+    __syncthreads();
+    block_exclusive_scan(cnt, pl.nseg, wsum);
+    __syncthreads();
+    block_exclusive_scan(pst, pl.nseg, wsum);
+    __syncthreads();
+    const uint32_t per = K > 0 ? (uint32_t)K : pl.k;
+    // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
+    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(rounds_max(K) * K) : (uint32_t)kStash;
+#pragma unroll
+    for (uint32_t t = 0; t < kNsMax; t += 8) {
+        if (t >= ns) break;
+        uint32_t pos[8], val[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
+            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> kSegBits], 1u) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (val[q] != kSentinel) {
+                const uint32_t local = ((t + q) / per) * kPBlock + tid;  // round r = slot / k
+                ent[pos[q]] = (local << kSegBits) | (val[q] & kOffMask);
+            }
+    }
+    __syncthreads();
+    // runs -> global, padded to multiples of 8; 8-lane groups, one run at a time
+    const uint32_t grp = tid >> 3, q = tid & 7;
+    uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.cap;
+    uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nseg;
+    for (uint32_t s = grp; s < pl.nseg; s += kPBlock / 8) {
+        const uint32_t st = s ? cnt[s - 1] : 0, en = cnt[s], c = en - st, pc = (c + 7) & ~7u;
+        const uint32_t d = pst[s];
+        for (uint32_t x = q; x < pc; x += 8) out[d + x] = ent[std::min(st + x, en - 1)];
+        if (q == 0) eo[s] = (uint16_t)(d + pc);
+    }
+}
+
+// Q3 variants (VBF_Q3, speed only; identical answers):
+//   0: one pass per 8-lane group and tile, 8 tiles per wave-step
+//   1: the k_seg_or<3> scheme -- a wave serves 8 * NG tiles per batch, run bounds loaded
+//      coalesced and spread with ds_bpermute, bounds of b+2 / entries of b+1 / bit tests of b in
+//      flight together, unconditional entry loads (idle lanes re-read their run's start)
+template <int V, int NG = 4>
+__global__ __launch_bounds__(kPBlock) void k_probe_seg(const uint32_t* tiles, const uint16_t* endsT, uint32_t ntiles,
+                                                       ProbePlan pl, uint32_t G, const uint32_t* words, uint8_t* res) {
+    __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
+    const uint32_t nwg = gridDim.x, qq = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+    const uint32_t wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + blockIdx.x / 8;
+    const uint32_t seg = wg / G, part = wg % G;  // several workgroups per segment when segments are few
+    const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / G), t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / G);
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t wbase = (uint64_t)seg * kSegWords;
+    const uint32_t wn = (uint32_t)std::min<uint64_t>(kSegWords, pl.nwords - wbase);
+    for (uint32_t w = tid * 4; w < kSegWords; w += kPBlock * 4) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (w + 4 <= wn) {
+            v = *reinterpret_cast<const uint4*>(words + wbase + w);
+        } else if (w < wn) {
+            v.x = words[wbase + w];
+            if (w + 1 < wn) v.y = words[wbase + w + 1];
+            if (w + 2 < wn) v.z = words[wbase + w + 2];
+        }
+        *reinterpret_cast<uint4*>(bitmap + w) = v;
+    }
+    __syncthreads();
+    const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
+    const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * ntiles : nullptr;
+    const uint32_t grp = lane >> 3, q8 = (lane & 7) * 8;
+    // 8 entries -> 1 result byte (bit c = entry c's filter bit)
+    auto test8 = [&](const uint4& a, const uint4& b) -> uint32_t {
+        const uint32_t e[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t r = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t off = e[c] & kOffMask;
+            r |= ((bitmap[off >> 5] >> (off & 31)) & 1u) << c;
+        }
+        return r;
+    };
+    if constexpr (V == 1) {
+        const uint32_t step = (kPBlock / 64) * 8 * NG;
+        uint32_t tg = t_lo + wave * 8 * NG;
+        auto lb = [&](uint32_t t0) -> uint32_t {
+            const uint32_t t = t0 + lane;
+            uint32_t v = 0;
+            if (t < t_hi) v = (row_beg ? (uint32_t)row_beg[t] : 0u) | ((uint32_t)row_end[t] << 16);
+            return v;
+        };
+        struct Batch {
+            uint32_t be[NG];
+            uint4 a[NG], b[NG];
+        };
+        auto spread = [&](uint32_t v, Batch& bt) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) bt.be[g] = (uint32_t)__shfl((int)v, g * 8 + grp);
+        };
+        auto issue = [&](uint32_t t0, Batch& bt) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const uint32_t st = bt.be[g] & 0xFFFFu, len = (bt.be[g] >> 16) - st;
+                const uint32_t t = std::min(t0 + g * 8 + grp, t_hi - 1);
+                const uint32_t x = q8 < len ? st + q8 : st;
+                const uint32_t* run = tiles + (uint64_t)t * pl.cap + x;
+                bt.a[g] = *reinterpret_cast<const uint4*>(run);
+                bt.b[g] = *reinterpret_cast<const uint4*>(run + 4);
+            }
+        };
+        auto consume = [&](uint32_t t0, const Batch& bt) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const uint32_t st = bt.be[g] & 0xFFFFu, len = (bt.be[g] >> 16) - st;
+                const uint64_t t = t0 + g * 8 + grp;
+                if (q8 < len) res[(t * pl.cap + st + q8) >> 3] = (uint8_t)test8(bt.a[g], bt.b[g]);
+            }
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {  // runs longer than 64 entries
+                const uint32_t st = bt.be[g] & 0xFFFFu, len = (bt.be[g] >> 16) - st;
+                const uint64_t t = t0 + g * 8 + grp;
+#pragma unroll 1
+                for (uint32_t x = st + q8 + 64; x < st + len; x += 64) {
+                    const uint32_t* run = tiles + t * pl.cap + x;
+                    res[(t * pl.cap + x) >> 3] =
+                        (uint8_t)test8(*reinterpret_cast<const uint4*>(run), *reinterpret_cast<const uint4*>(run + 4));
+                }
+            }
+        };
+        Batch A, B;
+        uint32_t v0 = lb(tg), v1 = lb(tg + step);
+        spread(v0, A);
+        if (tg < t_hi) issue(tg, A);
+        while (tg < t_hi) {
+            spread(v1, B);
+            uint32_t v2 = lb(tg + 2 * step);
+            const bool more = tg + step < t_hi;
+            if (more) issue(tg + step, B);
+            consume(tg, A);
+            tg += step;
+            if (!more) break;
+            v1 = v2;
+            spread(v1, A);
+            v2 = lb(tg + 2 * step);
+            const bool more2 = tg + step < t_hi;
+            if (more2) issue(tg + step, A);
+            consume(tg, B);
+            tg += step;
+            if (!more2) break;
+            v1 = v2;
+        }
+    } else {
+        // 8-lane group per tile, 8 tiles per wave-step: each lane tests 8 entries -> 1 byte
+        for (uint32_t t = t_lo + wave * 8 + grp; t < t_hi; t += (kPBlock / 64) * 8) {
+            const uint32_t beg = row_beg ? row_beg[t] : 0, end = row_end[t];
+            const uint32_t* run = tiles + (uint64_t)t * pl.cap;
+            for (uint32_t x = beg + q8; x < end; x += 64) {
+                const uint4 a = *reinterpret_cast<const uint4*>(run + x);
+                const uint4 b = *reinterpret_cast<const uint4*>(run + x + 4);
+                res[((uint64_t)t * pl.cap + x) >> 3] = (uint8_t)test8(a, b);
+            }
+        }
+    }
+}
+
+// OUT: 0 answer bytes, 1 hit count.
+template <int OUT>
+__global__ __launch_bounds__(kPBlock) void k_probe_out(const uint32_t* tiles, const uint16_t* ends, const uint8_t* res,
+                                                       ProbePlan pl, uint64_t n, uint8_t* out, uint32_t* partial) {
+    __shared__ uint32_t ok[4096 / 32];
+    __shared__ uint32_t wsum[kPBlock / 64];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
+    const uint32_t nk = (uint32_t)std::min<uint64_t>(pl.KT, n - key0);
+    for (uint32_t w = tid; w < (nk + 31) / 32; w += kPBlock) ok[w] = 0xFFFFFFFFu;
+    __syncthreads();
+    const uint32_t total = ends[(uint64_t)blockIdx.x * pl.nseg + pl.nseg - 1];
+    const uint32_t* tl = tiles + (uint64_t)blockIdx.x * pl.cap;
+    // 32 result bits per lane (cap is a multiple of 32, so each tile's bytes are dword aligned);
+    // only the clear bits -- entries whose filter bit is 0 -- cost a tile read and an LDS AND
+    const uint32_t* rs = reinterpret_cast<const uint32_t*>(res + ((uint64_t)blockIdx.x * pl.cap >> 3));
+    for (uint32_t w = tid; w * 32 < total; w += kPBlock) {
+        const uint32_t valid = std::min<uint32_t>(32, total - w * 32);
+        uint32_t z = ~rs[w];
+        if (valid < 32) z &= (1u << valid) - 1u;
+        while (z) {
+            const uint32_t c = __builtin_ctz(z);
+            z &= z - 1;
+            const uint32_t local = tl[w * 32 + c] >> kSegBits;
+            atomicAnd(&ok[local >> 5], ~(1u << (local & 31)));
+        }
+    }
+    __syncthreads();
+    if constexpr (OUT == 0) {
+        for (uint32_t l = tid; l < nk; l += kPBlock) out[key0 + l] = (ok[l >> 5] >> (l & 31)) & 1u;
+    } else {  // hits of the tile -> partial[tile] (summed by one finishing workgroup)
+        uint32_t c = 0;
+        for (uint32_t w = tid; w < (nk + 31) / 32; w += kPBlock) {
+            const uint32_t valid = (w + 1) * 32 <= nk ? 0xFFFFFFFFu : ((1u << (nk & 31)) - 1u);
+            c += __popc(ok[w] & valid);
+        }
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o);
+        if ((tid & 63) == 0) wsum[tid >> 6] = c;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < kPBlock / 64; ++w) t += wsum[w];
+            partial[blockIdx.x] = t;
+        }
+    }
+}
+
+static ProbePlan make_probe_plan(uint32_t m, uint32_t k) {
+    ProbePlan pl{};
+    pl.k = k;
+    pl.m = m;
+    pl.mu = ~0ull / m;
+    pl.nwords = ((uint64_t)m + 31) / 32;
+    pl.nseg = (uint32_t)(((uint64_t)m + (1u << kSegBits) - 1) >> kSegBits);
+    pl.nseg_pad = (pl.nseg + 3) & ~3u;
+    const uint32_t rmax = (uint32_t)rounds_max((int)k);
+    const int64_t avail = (int64_t)(kLdsPerCu / 2) - 64 - 8 * (int64_t)pl.nseg_pad;
+    const int64_t kt = std::min<int64_t>(std::min<int64_t>((int64_t)rmax * kPBlock, avail / 4 / k), 4096);
+    pl.KT = (uint32_t)std::max<int64_t>(kt, 1);
+    pl.R = (pl.KT + kPBlock - 1) / kPBlock;
+    pl.C = pl.KT * k;
+    pl.cap = (pl.C + 7 * pl.nseg + 31) & ~31u;  // multiple of 32: k_probe_out reads result dwords
+    pl.lds1 = (pl.C + 2 * pl.nseg_pad + 16) * 4;
+    return pl;
+}
+
+bool probe_partition_supported(uint32_t m, uint32_t k) {
+    if (m == 0 || k < 1 || k > (uint32_t)kStash) return false;
+    const ProbePlan pl = make_probe_plan(m, k);
+    return pl.KT >= 64 && pl.lds1 <= kLdsPerCu / 2 && pl.cap <= 65535;
+}
+
+static uint64_t probe_chunk_keys(const ProbePlan& pl, uint64_t n) {
+    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, kPartChunkIdx / pl.C);
+    return std::min<uint64_t>(n, tiles_per_chunk * pl.KT);
+}
+
+uint64_t probe_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
+    if (!probe_partition_supported(m, k)) return 0;
+    const ProbePlan pl = make_probe_plan(m, k);
+    const uint64_t ntiles = (probe_chunk_keys(pl, n) + pl.KT - 1) / pl.KT;
+    return ntiles * ((uint64_t)pl.cap * 4 + pl.cap / 8 + (uint64_t)pl.nseg * 4 + 4) + 1024;
+}
+
+uint64_t probe_count_partials(uint64_t n, uint32_t m, uint32_t k) {
+    const ProbePlan pl = make_probe_plan(m, k);
+    return (probe_chunk_keys(pl, n) + pl.KT - 1) / pl.KT;
+}
+
+hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                                    unsigned long long* count, void* ws, uint64_t ws_bytes, hipStream_t s) {
+    if (kb.n == 0) return hipSuccess;
+    if (!probe_partition_supported(m, k)) return hipErrorInvalidValue;
+    const ProbePlan pl = make_probe_plan(m, k);
+    const uint64_t chunk_keys = probe_chunk_keys(pl, kb.n);
+    const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
+    if (ws_bytes < probe_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;
+    auto align16 = [](uint64_t x) { return (x + 15) & ~15ull; };
+    char* base = static_cast<char*>(ws);
+    uint32_t* tiles = reinterpret_cast<uint32_t*>(base);
+    const uint64_t o_res = align16(max_tiles * pl.cap * 4);
+    const uint64_t o_ends = align16(o_res + max_tiles * pl.cap / 8);
+    const uint64_t o_endsT = align16(o_ends + max_tiles * pl.nseg * 2);
+    const uint64_t o_part = align16(o_endsT + max_tiles * pl.nseg * 2);
+    uint32_t* partial = reinterpret_cast<uint32_t*>(base + o_part);
+    uint8_t* res = reinterpret_cast<uint8_t*>(base + o_res);
+    uint16_t* ends = reinterpret_cast<uint16_t*>(base + o_ends);
+    uint16_t* endsT = reinterpret_cast<uint16_t*>(base + o_endsT);
+    for (uint64_t lo = 0; lo < kb.n; lo += chunk_keys) {
+        const uint64_t cn = std::min<uint64_t>(chunk_keys, kb.n - lo);
+        DevKeys dk{kb.keys, kb.offsets, kb.off_base, kb.stride, cn};
+        if (kb.offsets)
+            dk.offsets = kb.offsets + lo;
+        else
+            dk.keys = kb.keys + lo * kb.stride;
+        const uint32_t ntiles = (uint32_t)((cn + pl.KT - 1) / pl.KT);
+        hipError_t err = hipSuccess;
+        phase_begin(kPhaseProbePack, s);
+        with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
+            auto pick = [&]<bool S>() {
+                return k == 10 ? k_probe_pack<FMT, LP, 10, S>
+                     : k == 4  ? k_probe_pack<FMT, LP, 4, S>
+                     : k == 19 ? k_probe_pack<FMT, LP, 19, S>  // the reference's default p = 1e-4
+                               : k_probe_pack<FMT, LP, 0, false>;
+            };
+            auto fn = m <= (1u << 31) ? pick.template operator()<true>() : pick.template operator()<false>();
+            err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
+            if (err == hipSuccess)
+                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
+        });
+        if (err != hipSuccess) return err;
+        launch_transpose_u16(ends, endsT, ntiles, pl.nseg, s);
+        phase_end(kPhaseProbePack, s);
+        phase_begin(kPhaseProbeSeg, s);
+        const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
+        static const int q3v = [] { const char* e = getenv("VBF_Q3"); return e ? atoi(e) : 1; }();
+        hipLaunchKernelGGL(q3v == 1 ? k_probe_seg<1> : k_probe_seg<0>, dim3(pl.nseg * G), dim3(kPBlock), 0, s, tiles,
+                           endsT, ntiles, pl, G, words,
+                           res);
+        phase_end(kPhaseProbeSeg, s);
+        phase_begin(kPhaseProbeOut, s);
+        if (count) {
+            hipLaunchKernelGGL(k_probe_out<1>, dim3(ntiles), dim3(kPBlock), 0, s, tiles, ends, res, pl, cn, nullptr,
+                               partial);
+            err = launch_count_finish(partial, ntiles, count, s);
+            if (err != hipSuccess) return err;
+        } else {
+            hipLaunchKernelGGL(k_probe_out<0>, dim3(ntiles), dim3(kPBlock), 0, s, tiles, ends, res, pl, cn, out + lo,
+                               nullptr);
+        }
+        phase_end(kPhaseProbeOut, s);
+        err = hipGetLastError();
+        if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
+}
+
+}  // namespace vbf
