@@ -6,8 +6,11 @@
 // The bracketed length block is present for byte keys (`Hash for [u8]`, every production call
 // site); callers that pre-encode integer keys pass len_prefix = 0.
 //
-// On the 32-bit VALU a 64-bit add is v_add_co/v_addc (2 ops), a rotate by 13/16/17/21 is two
-// v_alignbit_b32, and a rotate by 32 is a register rename, so one SipRound is ~24 VALU ops.
+// On gfx950 a 64-bit add is one v_lshl_add_u64, a rotate by 13/16/17/21 two v_alignbit_b32 (both
+// half-rate: ~4.3 cycles per wave-instruction per SIMD against ~2.4-2.9 for v_xor / v_mov,
+// tools/isa_rate), and a rotate by 32 a register rename -- plus two v_mov when the swapped value
+// next feeds a v_lshl_add_u64, whose operands must sit in aligned register pairs.  One SipRound
+// is ~24 VALU instructions, ~80 SIMD cycles per wave.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

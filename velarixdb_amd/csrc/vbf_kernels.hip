@@ -43,7 +43,7 @@ struct Args {
 constexpr int kBlock = 256;
 
 // The per-key action, given a callable hash(i) for seeds i = 0..k-1.  Returns the probe answer.
-template <Op OP, class H>
+template <Op OP, bool M31, class H>
 __device__ __forceinline__ bool act(const Args& a, uint64_t j, const H& hash) {
     if constexpr (OP == Op::Build) {
         for (uint32_t i = 0; i < a.k; ++i) {
@@ -57,7 +57,7 @@ __device__ __forceinline__ bool act(const Args& a, uint64_t j, const H& hash) {
     } else {
         bool hit = true;  // k == 0 -> vacuously true (bf.rs:104)
         for (uint32_t i = 0; i < a.k; ++i) {
-            const uint32_t idx = fast_mod(hash(i), a.m, a.mu);
+            const uint32_t idx = mod_m<M31>(hash(i), a.m, a.mu);
             if (!((a.rwords[idx >> 5] >> (idx & 31)) & 1u)) {  // bf.rs:100-102 early exit
                 hit = false;
                 break;
@@ -109,14 +109,14 @@ hipError_t launch_count_finish(const uint32_t* partial, uint64_t np, unsigned lo
 uint64_t count_partials(uint64_t n) { return (n + kBlock - 1) / kBlock + 2; }
 
 // ---- one lane per key, any layout (keyhash.hpp) ----
-template <Op OP, int FMT, bool LP>
+template <Op OP, int FMT, bool LP, bool M31>
 __global__ __launch_bounds__(kBlock) void k_keys(Args a) {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool hit = false;
     if (j < a.n) {
         const DevKeys dk{a.keys, a.offsets, a.off_base, a.stride, a.n};
         const Prefix p = key_prefix<FMT, LP>(dk, j);
-        hit = act<OP>(a, j, [&](uint32_t i) { return prefix_hash(p, i); });
+        hit = act<OP, M31>(a, j, [&](uint32_t i) { return prefix_hash(p, i); });
     }
     finish_count<OP>(a, hit);
 }
@@ -127,7 +127,12 @@ template <Op OP>
 static void dispatch(const Args& a, bool lp, hipStream_t s) {
     const uint64_t blocks = (a.n + kBlock - 1) / kBlock;
     with_fmt(pick_fmt(a.keys, a.offsets, a.stride), lp, [&]<int FMT, bool LP>() {
-        hipLaunchKernelGGL((k_keys<OP, FMT, LP>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+        // probes with m <= 2^31: the one-word remainder (sip13.hpp fast_mod31) on the lookup chain
+        constexpr bool kProbe = OP == Op::Probe || OP == Op::Count;
+        if (kProbe && a.m <= (1ull << 31))
+            hipLaunchKernelGGL((k_keys<OP, FMT, LP, kProbe>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_keys<OP, FMT, LP, false>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);
     });
 }
 

@@ -68,7 +68,8 @@ __global__ __launch_bounds__(256) void k_multi_probe(MultiArgs a) {
         }
         if (hit) {  // bf.rs:95-105, k == 0 -> true
             for (uint32_t i = 0; i < d.k; ++i) {
-                const uint32_t idx = fast_mod(hash(i), d.m, d.mu);
+                const uint64_t h = hash(i);  // per-table m: a wave-uniform choice of remainder code
+                const uint32_t idx = d.m <= (1ull << 31) ? fast_mod31(h, (uint32_t)d.m, d.mu) : fast_mod(h, d.m, d.mu);
                 if (!((d.words[idx >> 5] >> (idx & 31)) & 1u)) {
                     hit = false;
                     break;
