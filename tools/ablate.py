@@ -40,7 +40,7 @@ print(json.dumps({p: round(ms / max(c, 1), 3) for p, (ms, c) in ph.items() if c}
 """
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for a in ("0", "1", "2", "3", "4", "5", "6", "7"):
+for a in (sys.argv[1:] or ["0", "1", "2", "3", "4", "5", "6", "7"]):
     lib = os.path.join(root, "velarixdb_amd", "libvbf_ablate.so")  # build.py --ablation
     if not os.path.exists(lib):
         sys.exit("missing %s: run `python velarixdb_amd/build.py --ablation` first" % lib)

@@ -420,14 +420,19 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
                 const uint32_t t = std::min(t0 + g * 8 + grp, t_hi - 1);
                 // idle lanes re-read the run's first 8 entries (same lines, always in bounds)
                 const uint32_t e = q8 < len ? st + q8 : st;
-                load8(tiles + (uint64_t)t * pl.tile_words, pl.CP, e, b.l[g], b.nib[g]);
+                if (VBF_ABLATION_BUILD && pl.ablate == 4) {  // timing experiment: no tile loads
+                    b.l[g] = make_uint4(t * 2654435761u + g, lane * 40503u, t ^ lane, e * 977u);
+                    b.nib[g] = t + lane;
+                } else {
+                    load8(tiles + (uint64_t)t * pl.tile_words, pl.CP, e, b.l[g], b.nib[g]);
+                }
             }
         };
         auto consume = [&](uint32_t t0, const Batch& b) {
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
                 const uint32_t st = b.be[g] & 0xFFFFu, len = (b.be[g] >> 16) - st;
-                if (q8 < len) or8(bitmap, b.l[g], b.nib[g], std::min<uint32_t>(8, len - q8));
+                if (q8 < len) or8(bitmap, b.l[g], b.nib[g], std::min<uint32_t>(8, len - q8), VBF_ABLATION_BUILD ? pl.ablate : 0);
             }
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
