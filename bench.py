@@ -33,7 +33,7 @@ from velarixdb_amd._lib import call  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32 lane-ops/s)
 # VALU lane-instructions per key of the build, from rocprofv3 SQ_INSTS_VALU (profiles/r01)
-VALU_PER_KEY_CFG2 = 1706.0
+VALU_PER_KEY_CFG2 = 1611.0
 
 
 def pmc_traffic(name):
@@ -208,7 +208,7 @@ def bench_fixed(ctx, args):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "build (all phases of one vbf_build_dev_ex launch)", "kernel_ms": kavg * 1e3,
-                     "rocprof_kernels": {"tile_sort": "k_tile_pack<16, true, 10>", "transpose": "k_transpose_u16",
+                     "rocprof_kernels": {"tile_sort": "k_tile_pack<16, true, 10, true>", "transpose": "k_transpose_u16",
                                          "seg_or": "k_seg_or<3, 1024, 5>"},
                      "rocprof_summary": "profiles/r01/bench_default_kernel_stats.csv",
                      "valu_frac_est": n * VALU_PER_KEY_CFG2 / kavg / VALU_PEAK_LANE_OPS,
