@@ -60,10 +60,19 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # Rehearsal knobs for the N>1 path on a one-GPU box: VBF_SHARE_DEVICE=1 puts every rank
+        # on cuda:0, VBF_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU).
+        # The driver's multi-GPU runs set neither: one rank per GPU over RCCL.
+        if os.environ.get("VBF_SHARE_DEVICE") == "1":
+            self.local = 0
+        self.backend = os.environ.get("VBF_DIST_BACKEND", "nccl")
         torch.cuda.set_device(self.local)
         self.dev = torch.device("cuda", self.local)
         if self.world > 1:
-            dist.init_process_group("nccl", device_id=self.dev)
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(self.backend)
         self.stream = torch.cuda.current_stream(self.dev)
         self.sp = ctypes.c_void_p(self.stream.cuda_stream)
 
@@ -74,14 +83,14 @@ class Ctx:
     def max_over_ranks(self, x):
         if self.world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev if self.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum_over_ranks(self, x):
         if self.world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        t = torch.tensor([x], dtype=torch.float64, device=self.dev if self.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 

@@ -39,6 +39,7 @@ for s in $STEPS; do
     compact) run bench_compact 600 python bench.py --compact --steps 5 --warmup 1 ;;
     multi)  run bench_multi 600 python bench.py --multi --steps 5 --warmup 1 ;;
     e2e)    run bench_e2e 600 python bench.py --e2e --steps 3 --warmup 1 ;;
+    dist2)  run bench_dist2 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;
     ubench) run ubench 300 ./tools/ubench ;;
     counters) (cd /tmp && run counters 120 rocprofv3 -L) || exit $? ;;
     pmc1) (cd /tmp && run pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc1" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
