@@ -73,9 +73,11 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
 }
 
 // K > 0: k known at compile time (the stash and seed loops unroll, no indexed register moves);
-// K == 0: any k <= kStash at run time.
+// K == 0: any k <= kStash at run time.  __launch_bounds__(1024, 8): two workgroups per CU (the
+// hashing of one overlaps the other's sort), i.e. at most 64 VGPRs; the offsets-layout kernels
+// would otherwise take 80-90 and drop to one workgroup per CU.
 template <int FMT, bool LP, int K, bool M31>
-__global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, uint32_t* tiles,
+__global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan pl, uint32_t* tiles,
                                                        uint16_t* ends) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // CP entries
@@ -105,8 +107,12 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
     uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     if constexpr (K > 0) {
         constexpr int RM = build_rounds_max(K);
-#pragma unroll
-        for (int r = 0; r < RM; ++r) {
+        // One instance per round with r a compile-time constant: the stash index r*K+i stays
+        // static even where the round body holds a runtime loop (the offsets layout's absorb),
+        // which keeps LLVM from unrolling a plain `for` -- the stash then went to scratch
+        // memory (128 B per lane of scratch stores and loads per key, variable-length builds).
+        auto round = [&](auto rc) {
+            constexpr int r = decltype(rc)::value;
             const uint32_t slot = (uint32_t)r * kPBlock + tid;
             const bool valid = (uint32_t)r < pl.R && slot < nk;
             Prefix p{};
@@ -120,7 +126,10 @@ __global__ __launch_bounds__(kPBlock) void k_tile_pack(DevKeys dk, PartPlan pl, 
                 }
                 stash[r * K + i] = idx;
             }
-        }
+        };
+        [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
+            (round(std::integral_constant<int, Rs>{}), ...);
+        }(std::make_integer_sequence<int, RM>{});
         ns = RM * K;
     } else {
         ns = 0;

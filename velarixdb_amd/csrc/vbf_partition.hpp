@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <utility>
 
 #include "keyhash.hpp"
 #include "sip13.hpp"

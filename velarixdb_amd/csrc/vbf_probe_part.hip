@@ -26,7 +26,7 @@ constexpr uint32_t kOffMask = (1u << kSegBits) - 1;
 static_assert(kSegBits == 20, "probe entries hold a 12-bit key id above the 20-bit offset");
 
 template <int FMT, bool LP, int K, bool M31>
-__global__ __launch_bounds__(kPBlock) void k_probe_pack(DevKeys dk, ProbePlan pl, uint32_t* tiles, uint16_t* ends) {
+__global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan pl, uint32_t* tiles, uint16_t* ends) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* ent = smem;               // C entries
     uint32_t* cnt = ent + pl.C;         // nseg_pad: counts -> starts -> ends
@@ -41,8 +41,9 @@ __global__ __launch_bounds__(kPBlock) void k_probe_pack(DevKeys dk, ProbePlan pl
     uint32_t ns;
     if constexpr (K > 0) {
         constexpr int RM = rounds_max(K);
-#pragma unroll
-        for (int r = 0; r < RM; ++r) {
+        // compile-time r per round (see k_tile_pack): keeps the stash out of scratch memory
+        auto round = [&](auto rc) {
+            constexpr int r = decltype(rc)::value;
             const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
             const bool valid = (uint32_t)r < pl.R && j < key_end;
             Prefix p{};
@@ -56,7 +57,10 @@ __global__ __launch_bounds__(kPBlock) void k_probe_pack(DevKeys dk, ProbePlan pl
                 }
                 stash[r * K + i] = idx;
             }
-        }
+        };
+        [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
+            (round(std::integral_constant<int, Rs>{}), ...);
+        }(std::make_integer_sequence<int, RM>{});
         ns = RM * K;
     } else {
         ns = 0;
