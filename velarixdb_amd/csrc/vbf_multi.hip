@@ -44,20 +44,11 @@ __global__ __launch_bounds__(256) void k_multi_probe(MultiArgs a) {
         kl = a.stride;
     }
     const Prefix p = key_prefix<FMT, LP>(dk, j);
+    // Seed hashes 0..3 are formed once, on the first table whose range holds the key, and kept
+    // in named registers: a memo indexed by the runtime seed number was lowered to a scratch
+    // array (a scratch load per bit test).
     uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    uint32_t have = 0;
-    auto hash = [&](uint32_t i) -> uint64_t {
-        if (i >= 4) return prefix_hash(p, i);
-        if (!((have >> i) & 1u)) {
-            const uint64_t v = prefix_hash(p, i);
-            if (i == 0) h0 = v;
-            else if (i == 1) h1 = v;
-            else if (i == 2) h2 = v;
-            else h3 = v;
-            have |= 1u << i;
-        }
-        return i == 0 ? h0 : i == 1 ? h1 : i == 2 ? h2 : h3;
-    };
+    bool have = false;
     uint8_t* out = a.out + j * a.nsst;
     for (uint32_t s = 0; s < a.nsst; ++s) {
         const MultiSst d = a.tab[s];
@@ -66,15 +57,20 @@ __global__ __launch_bounds__(256) void k_multi_probe(MultiArgs a) {
             hit = cmp_bytes(kp, kl, a.bounds + d.lo_beg, d.lo_end - d.lo_beg) >= 0 &&
                   cmp_bytes(kp, kl, a.bounds + d.hi_beg, d.hi_end - d.hi_beg) <= 0;
         }
-        if (hit) {  // bf.rs:95-105, k == 0 -> true
-            for (uint32_t i = 0; i < d.k; ++i) {
-                const uint64_t h = hash(i);  // per-table m: a wave-uniform choice of remainder code
-                const uint32_t idx = d.m <= (1ull << 31) ? fast_mod31(h, (uint32_t)d.m, d.mu) : fast_mod(h, d.m, d.mu);
-                if (!((d.words[idx >> 5] >> (idx & 31)) & 1u)) {
-                    hit = false;
-                    break;
-                }
+        if (hit && d.k > 0) {  // bf.rs:95-105, k == 0 -> true; early exit on the first clear bit
+            if (!have) {
+                h0 = prefix_hash(p, 0);
+                h1 = prefix_hash(p, 1);
+                h2 = prefix_hash(p, 2);
+                h3 = prefix_hash(p, 3);
+                have = true;
             }
+            auto test = [&](uint64_t h) -> bool {  // per-table m: a wave-uniform choice of remainder code
+                const uint32_t idx = d.m <= (1ull << 31) ? fast_mod31(h, (uint32_t)d.m, d.mu) : fast_mod(h, d.m, d.mu);
+                return (d.words[idx >> 5] >> (idx & 31)) & 1u;
+            };
+            hit = test(h0) && (d.k < 2 || test(h1)) && (d.k < 3 || test(h2)) && (d.k < 4 || test(h3));
+            for (uint32_t i = 4; hit && i < d.k; ++i) hit = test(prefix_hash(p, i));
         }
         out[s] = hit ? 1 : 0;
     }
