@@ -34,6 +34,8 @@ for s in $STEPS; do
     probephases) run probe_phases 300 python tools/probe_phases.py ;;
     benchatomic) run bench_atomic 300 python bench.py --no-cpu-baseline --strategy 1 --steps 3 ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
+    bench3q) run bench_cfg3q 600 python bench.py --config 3 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    bench3nolo) run bench_cfg3_nolo 600 env VBF_LEN_ORDER=0 python bench.py --config 3 --steps 5 --warmup 1 --no-cpu-baseline ;;
     bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;
     sst)    run bench_sst 600 python bench.py --sst --steps 5 --warmup 1 ;;
     compact) run bench_compact 600 python bench.py --compact --steps 5 --warmup 1 ;;

@@ -38,6 +38,7 @@ struct PartPlan {
     uint32_t stagger_lo, stagger_hi, stagger_sleeps;
     uint32_t ablate;      // ablation builds only (VBF_ABLATE, vbf_kernels.hpp): 1 skip place+copy
     uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or); 0 = by run length
+    uint32_t len_order;   // offsets layout: deal keys to lanes by length (VBF_LEN_ORDER, default 1)
     uint64_t m, mu, nwords;
 };
 
@@ -102,8 +103,11 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
     const uint32_t nk = (uint32_t)(key_end - key0);
     // perm lives in the (not yet used) tile image; every read of it precedes the barrier below
-    if constexpr (FMT < 0) length_order(dk, key0, nk, lo, lhist);
-    auto key_of = [&](uint32_t slot) -> uint64_t { return key0 + (FMT < 0 ? (uint32_t)lo[slot] : slot); };
+    const bool perm = FMT < 0 && pl.len_order;
+    if constexpr (FMT < 0) {
+        if (perm) length_order(dk, key0, nk, lo, lhist);
+    }
+    auto key_of = [&](uint32_t slot) -> uint64_t { return key0 + (perm ? (uint32_t)lo[slot] : slot); };
     uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     if constexpr (K > 0) {
         constexpr int RM = build_rounds_max(K);
@@ -582,6 +586,8 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.ablate = (uint32_t)abl;
     static const int k3v = [] { const char* e = getenv("VBF_K3"); return e ? atoi(e) : 0; }();
     pl.k3v = (uint32_t)k3v;
+    static const int lord = [] { const char* e = getenv("VBF_LEN_ORDER"); return e ? atoi(e) : 1; }();
+    pl.len_order = (uint32_t)(lord != 0);
     return pl;
 }
 
