@@ -36,6 +36,7 @@ for s in $STEPS; do
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;
     bench3q) run bench_cfg3q 600 python bench.py --config 3 --steps 5 --warmup 1 --no-cpu-baseline ;;
     bench3nolo) run bench_cfg3_nolo 600 env VBF_LEN_ORDER=0 python bench.py --config 3 --steps 5 --warmup 1 --no-cpu-baseline ;;
+    bench3nostage) run bench_cfg3_nostage 600 env VBF_STAGE_KEYS=0 python bench.py --config 3 --steps 5 --warmup 1 --no-cpu-baseline ;;
     bench5) run bench_cfg5 900 python bench.py --config 5 --steps 3 --warmup 1 ;;
     sst)    run bench_sst 600 python bench.py --sst --steps 5 --warmup 1 ;;
     compact) run bench_compact 600 python bench.py --compact --steps 5 --warmup 1 ;;

@@ -74,21 +74,12 @@ __device__ __forceinline__ Prefix absorb_fixed(const FixedWords<FMT>& kw) {
     return p;
 }
 
-template <int FMT, bool LP>
-__device__ __forceinline__ Prefix key_prefix(const DevKeys& a, uint64_t j) {
+// Any key given as (byte position in `keys`, length): the runtime-length absorb.
+template <bool LP>
+__device__ __forceinline__ Prefix key_prefix_at(const uint8_t* keys, uint64_t beg, uint64_t len) {
     Prefix p;
-    if constexpr (FMT > 0) {
-        p = absorb_fixed<FMT, LP>(load_fixed<FMT>(a, j));
-    } else {
-        uint64_t beg, len;
-        if constexpr (FMT < 0) {
-            beg = a.offsets[j] - a.off_base;
-            len = a.offsets[j + 1] - a.offsets[j];
-        } else {
-            beg = j * a.stride;
-            len = a.stride;
-        }
-        const uintptr_t addr = reinterpret_cast<uintptr_t>(a.keys + beg);
+    {
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(keys + beg);
         const uintptr_t end = addr + len;
         const uintptr_t wstart = addr & ~(uintptr_t)7;
         const uint64_t* wbase = reinterpret_cast<const uint64_t*>(wstart);
@@ -128,6 +119,17 @@ __device__ __forceinline__ Prefix key_prefix(const DevKeys& a, uint64_t j) {
         p.total = (uint32_t)((len + (LP ? 8 : 0) + 8) & 0xff);
     }
     return p;
+}
+
+template <int FMT, bool LP>
+__device__ __forceinline__ Prefix key_prefix(const DevKeys& a, uint64_t j) {
+    if constexpr (FMT > 0) {
+        return absorb_fixed<FMT, LP>(load_fixed<FMT>(a, j));
+    } else if constexpr (FMT < 0) {
+        return key_prefix_at<LP>(a.keys, a.offsets[j] - a.off_base, a.offsets[j + 1] - a.offsets[j]);
+    } else {
+        return key_prefix_at<LP>(a.keys, j * a.stride, a.stride);
+    }
 }
 
 // Host-side choice of FMT for a batch: the compile-time fixed layouts need aligned rows.

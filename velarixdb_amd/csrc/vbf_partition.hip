@@ -39,6 +39,7 @@ struct PartPlan {
     uint32_t ablate;      // ablation builds only (VBF_ABLATE, vbf_kernels.hpp): 1 skip place+copy
     uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or); 0 = by run length
     uint32_t len_order;   // offsets layout: deal keys to lanes by length (VBF_LEN_ORDER, default 1)
+    uint32_t stage_keys;  // the lo16 image holds perm + (begin, length) per key (VBF_STAGE_KEYS)
     uint64_t m, mu, nwords;
 };
 
@@ -49,8 +50,11 @@ struct PartPlan {
 // the order changes speed only.  hist[kLenBuckets] must be zero on entry; ends with a barrier.
 constexpr int kLenBuckets = 32;
 
+// With sbeg/slen (not null) the second pass also stages each key's (begin - base, length) at its
+// sorted slot, so the hashing rounds read them from LDS instead of a dependent offsets load.
 __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, uint32_t nk, uint16_t* perm,
-                                             uint32_t* hist) {
+                                             uint32_t* hist, uint32_t* sbeg = nullptr, uint32_t* slen = nullptr,
+                                             uint64_t base = 0) {
     const uint32_t tid = threadIdx.x;
     auto bucket = [&](uint32_t l) {
         const uint64_t len = dk.offsets[key0 + l + 1] - dk.offsets[key0 + l];
@@ -69,7 +73,15 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
         if (tid < kLenBuckets) hist[tid] = incl - v;
     }
     __syncthreads();
-    for (uint32_t l = tid; l < nk; l += kPBlock) perm[atomicAdd(&hist[bucket(l)], 1u)] = (uint16_t)l;
+    for (uint32_t l = tid; l < nk; l += kPBlock) {
+        const uint64_t b = dk.offsets[key0 + l], len = dk.offsets[key0 + l + 1] - b;
+        const uint32_t pos = atomicAdd(&hist[(uint32_t)std::min<uint64_t>(len >> 3, kLenBuckets - 1)], 1u);
+        perm[pos] = (uint16_t)l;
+        if (sbeg) {
+            sbeg[pos] = (uint32_t)(b - base);
+            slen[pos] = (uint32_t)len;
+        }
+    }
     __syncthreads();
 }
 
@@ -104,8 +116,22 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     const uint32_t nk = (uint32_t)(key_end - key0);
     // perm lives in the (not yet used) tile image; every read of it precedes the barrier below
     const bool perm = FMT < 0 && pl.len_order;
+    // Staged keys (offsets layout, compiled k, plan says the image holds perm + 2 words per key,
+    // and the tile's bytes span < 4 GiB): (begin, length) at smem[sw0 ..) and smem[sw0 + nk ..).
+    const uint32_t sw0 = (nk + 1) / 2;
+    bool staged = false;
+    uint64_t sbase = 0;
     if constexpr (FMT < 0) {
-        if (perm) length_order(dk, key0, nk, lo, lhist);
+        if (perm) {
+            if (K > 0 && pl.stage_keys) {
+                sbase = dk.offsets[key0];
+                staged = dk.offsets[key_end] - sbase < (1ull << 32);
+            }
+            if (staged)
+                length_order(dk, key0, nk, lo, lhist, smem + sw0, smem + sw0 + nk, sbase);
+            else
+                length_order(dk, key0, nk, lo, lhist);
+        }
     }
     auto key_of = [&](uint32_t slot) -> uint64_t { return key0 + (perm ? (uint32_t)lo[slot] : slot); };
     uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
@@ -120,7 +146,22 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
             const uint32_t slot = (uint32_t)r * kPBlock + tid;
             const bool valid = (uint32_t)r < pl.R && slot < nk;
             Prefix p{};
-            if (valid) p = key_prefix<FMT, LP>(dk, key_of(slot));
+            if (valid) {
+                if constexpr (FMT < 0) {
+                    uint64_t beg, len;
+                    if (staged) {
+                        beg = sbase - dk.off_base + smem[sw0 + slot];
+                        len = smem[sw0 + nk + slot];
+                    } else {
+                        const uint64_t j = key_of(slot);
+                        beg = dk.offsets[j] - dk.off_base;
+                        len = dk.offsets[j + 1] - dk.offsets[j];
+                    }
+                    p = key_prefix_at<LP>(dk.keys, beg, len);
+                } else {
+                    p = key_prefix<FMT, LP>(dk, key_of(slot));
+                }
+            }
 #pragma unroll
             for (int i = 0; i < K; ++i) {
                 uint32_t idx = kSentinel;
@@ -588,6 +629,9 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.k3v = (uint32_t)k3v;
     static const int lord = [] { const char* e = getenv("VBF_LEN_ORDER"); return e ? atoi(e) : 1; }();
     pl.len_order = (uint32_t)(lord != 0);
+    static const int stg = [] { const char* e = getenv("VBF_STAGE_KEYS"); return e ? atoi(e) : 1; }();
+    // words: perm (KT u16) + begin + length (KT u32 each) inside the CP/2 words of low halves
+    pl.stage_keys = (uint32_t)(stg != 0 && (uint64_t)(pl.KT + 1) / 2 + 2ull * pl.KT <= pl.CP / 2);
     return pl;
 }
 
