@@ -399,6 +399,46 @@ def test_product_library_ignores_ablation_env(vbf, tmp_path):
         assert r.returncode == 0 and "ok" in r.stdout, (a, r.stderr[-2000:])
 
 
+def test_variable_length_knobs_same_words(vbf, ora, tmp_path):
+    """The speed-only knobs of the variable-length partitioned build (VBF_LEN_ORDER: lanes in
+    length order or key order; VBF_STAGE_KEYS: (begin, length) staged in LDS or read from the
+    offsets) must give the oracle's words in every combination.  The library reads them once per
+    process, so each combination builds in a child process (vbf_build_host, AUTO: partitioned at
+    these sizes, >= 2^22 bit indices) and the parent checks the words against the oracle."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    from velarixdb_amd.keys import pack_offsets
+    from velarixdb_amd.workloads import SEED_CFG3, var_offsets
+    cases = ((2_000_003, 10), (3_800_000, 19), (900_001, 4))
+    n = 1_100_000
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import numpy as np, oracle as ora, velarixdb_amd as v\n"
+        "from velarixdb_amd.keys import pack_offsets\n"
+        "from velarixdb_amd.workloads import SEED_CFG3, var_offsets\n"
+        "off = var_offsets(SEED_CFG3, 7, %d)\n"
+        "b = pack_offsets(ora.gen_var(SEED_CFG3, 7, off), off)\n"
+        "for m, k in %r:\n"
+        "    w = np.zeros((m + 31) // 32, np.uint32)\n"
+        "    v._lib.call('vbf_build_host', b.data.ctypes.data, b.offsets.ctypes.data, 0, b.n, 1, m, k,\n"
+        "                w.ctypes.data, w.size, 0)\n"
+        "    np.save(sys.argv[1] + '_%%d.npy' %% k, w)\n"
+        "print('ok')\n" % (ROOT, n, cases))
+    off = var_offsets(SEED_CFG3, 7, n)
+    b = pack_offsets(ora.gen_var(SEED_CFG3, 7, off), off)
+    want = {k: ora.build_words(b, m, k, threads=8) for m, k in cases}
+    for lo, st in (("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")):
+        env = {kk: vv for kk, vv in os.environ.items() if kk != "VBF_LIB"}
+        env["VBF_LEN_ORDER"], env["VBF_STAGE_KEYS"] = lo, st
+        stem = str(tmp_path / ("w%s%s" % (lo, st)))
+        r = subprocess.run([sys.executable, "-c", code, stem], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0 and "ok" in r.stdout, (lo, st, r.stderr[-2000:])
+        for m, k in cases:
+            assert np.array_equal(np.load(stem + "_%d.npy" % k), want[k]), (lo, st, m, k)
+
+
 @pytest.mark.parametrize("strategy", [1, 2])
 def test_concentrated_indices(vbf, ora, strategy):
     """Adversarial skew: 3M copies of three keys put every tile's 30K bit indices into a handful of
