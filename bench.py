@@ -2,11 +2,17 @@
 """Bloom-filter build benchmark on MI355X (BASELINE.json metric: build keys/s + key-bytes GiB/s,
 device-resident, 1/2/4/8 GPUs).
 
-Default workload (N=1): BASELINE config 2 -- 100M x 16-byte keys, 10 bits/key
+Default workload at N=1: BASELINE config 2 -- 100M x 16-byte keys, 10 bits/key
 (m = 1,000,000,000 bits, k = 10), keys already resident in HBM.  One step = BloomFilter::new's
 zeroed bit array (bf.rs:71) + build_filter_from_entries over the batch (bf.rs:126-128).
-With N > 1 (torchrun, one rank per GPU) every rank builds its own independent SSTable shard
-of the same size (config 4's compaction fan-in): weak scaling, no data-path collective.
+At N > 1 the default is BASELINE config 4, the compaction fan-in: every rank builds its own
+independent SSTable shard of 50M x 16-byte keys (m = 500,000,000, k = 10, seed 0x5EED0040 +
+rank), one filter per merged table as compactors/sized.rs:170-200 builds them (filter at
+:192-193).  Weak scaling, no data-path collective.
+
+`python bench.py --gpus N` with N > 1 and no launcher in the environment starts the N ranks
+itself (torch.distributed.run as a child process, before anything touches the GPU) and exits
+with their status.  Under a launcher, WORLD_SIZE must equal --gpus.
 
 Also: --config 3 (100M variable-length Zipf keys + 50M negative probes), --config 5 (1B x 32 B,
 15 bits/key -> m saturates at u32::MAX, k = 4; keys split over ranks, OR all-reduce, full
@@ -16,8 +22,82 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
+
+
+def make_parser():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="BASELINE config (default: 2 on one GPU, 4 on several)")
+    ap.add_argument("--keys", type=int, default=None)
+    ap.add_argument("--key-bytes", type=int, default=16)
+    ap.add_argument("--bits-per-key", type=int, default=10)
+    ap.add_argument("--neg-keys", type=int, default=None)
+    ap.add_argument("--e2e", action="store_true")
+    ap.add_argument("--sst", action="store_true", help="SST data.db decode + rebuild (8(f) row 2)")
+    ap.add_argument("--compact", action="store_true", help="compaction merge + filter (8(f) row 3)")
+    ap.add_argument("--multi", action="store_true", help="batched multi-SST probe (8(f) row 4)")
+    ap.add_argument("--memtable", action="store_true",
+                    help="single-key set/contains latency on a memtable-size filter (mem.rs:207-230)")
+    ap.add_argument("--strategy", type=int, default=0, help="0 auto, 1 atomic, 2 partitioned")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=10_000_000)
+    ap.add_argument("--cpu-opt-threads", type=int, default=None,
+                    help="threads of the prefix-shared CPU port (default: every usable host core)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="launch the ranks, report world size and each rank's workload, touch no GPU")
+    return ap
+
+
+def launch_plan(gpus, env):
+    """How this invocation runs: ("spawn", N) -- no launcher and --gpus N > 1, so start N ranks;
+    ("run", world) -- run this process as one rank of `world`.  A launcher's WORLD_SIZE that
+    disagrees with an explicit --gpus is an error (the driver's N must be the N measured)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        n = 1 if gpus is None else gpus
+        if n < 1:
+            raise ValueError("--gpus must be >= 1 (got %d)" % n)
+        return ("spawn", n) if n > 1 else ("run", 1)
+    world = int(ws)
+    if gpus is not None and gpus != world:
+        raise ValueError("--gpus %d but the launcher started WORLD_SIZE=%d ranks" % (gpus, world))
+    return ("run", world)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_command(nproc, argv, port):
+    """torch.distributed.run over this script, one rank per GPU, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def maybe_spawn_ranks():
+    """Runs before torch or libvbf touch the GPU: a child process, never an exec."""
+    args, _ = make_parser().parse_known_args()
+    mode, n = launch_plan(args.gpus, os.environ)
+    if mode == "spawn":
+        print("bench.py: starting %d ranks (torch.distributed.run, one per GPU)" % n, file=sys.stderr, flush=True)
+        rc = subprocess.call(spawn_command(n, sys.argv[1:], _free_port()))
+        sys.exit(rc)
+
+
+if __name__ == "__main__":
+    maybe_spawn_ranks()
 
 import numpy as np
 import torch
@@ -36,15 +116,24 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32
 VALU_PER_KEY_CFG2 = 1611.0
 
 
+# rocprofv3 names of the default build's kernels and the summary of the same command
+ROCPROF_KERNELS = {"tile_sort": "k_tile_pack<16, true, 10, true>", "transpose": "k_transpose_u16",
+                   "seg_or": "k_seg_or<3, 1024, 5>"}
+ROCPROF_SUMMARY = "profiles/r01/bench_default_kernel_stats.csv"
+
+
 def pmc_traffic(name):
-    """Per-launch HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes."""
-    path = os.path.join(ROOT, "profiles", "r01", name)
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        return d["per_launch_bytes"], "profiles/r01/" + name
-    except (OSError, ValueError, KeyError):
-        return None, None
+    """Per-launch HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes (the newest
+    round's measurement)."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", rnd, name)
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            return d["per_launch_bytes"], "profiles/%s/%s" % (rnd, name)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
 
 
 def vp(t):
@@ -60,12 +149,18 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
         # Rehearsal knobs for the N>1 path on a one-GPU box: VBF_SHARE_DEVICE=1 puts every rank
         # on cuda:0, VBF_DIST_BACKEND=gloo replaces RCCL (which refuses two ranks on one GPU).
         # The driver's multi-GPU runs set neither: one rank per GPU over RCCL.
-        if os.environ.get("VBF_SHARE_DEVICE") == "1":
+        self.shared_device = os.environ.get("VBF_SHARE_DEVICE") == "1"
+        if self.shared_device:
             self.local = 0
         self.backend = os.environ.get("VBF_DIST_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
+        if not self.shared_device and self.local_world > ndev:
+            raise SystemExit("bench.py: %d ranks on this node but only %d visible GPUs (one rank per GPU)"
+                             % (self.local_world, ndev))
         torch.cuda.set_device(self.local)
         self.dev = torch.device("cuda", self.local)
         if self.world > 1:
@@ -73,26 +168,65 @@ class Ctx:
                 dist.init_process_group("nccl", device_id=self.dev)
             else:
                 dist.init_process_group(self.backend)
+            assert dist.get_world_size() == self.world, (dist.get_world_size(), self.world)
         self.stream = torch.cuda.current_stream(self.dev)
         self.sp = ctypes.c_void_p(self.stream.cuda_stream)
+        self.topology = self._topology()
+
+    def _device_info(self):
+        p = torch.cuda.get_device_properties(self.dev)
+        pci = "%04x:%02x:%02x" % (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                                  getattr(p, "pci_device_id", 0))
+        return {"rank": self.rank, "local_rank": self.local, "device": self.local, "pci": pci,
+                "name": p.name, "arch": getattr(p, "gcnArchName", ""), "host": socket.gethostname()}
+
+    def _topology(self):
+        """Every rank's device; with one rank per GPU no two ranks may share a card."""
+        mine = self._device_info()
+        if self.world == 1:
+            return {"world_size": 1, "backend": None, "ranks": [mine]}
+        allr = [None] * self.world
+        dist.all_gather_object(allr, mine)
+        seen = {}
+        for r in allr:
+            key = (r["host"], r["pci"])
+            if key in seen and not self.shared_device:
+                raise SystemExit("bench.py: ranks %d and %d share GPU %s on %s" % (seen[key], r["rank"], r["pci"],
+                                                                                  r["host"]))
+            seen[key] = r["rank"]
+        topo = {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "ranks": allr,
+                "shared_device_rehearsal": self.shared_device}
+        if self.backend == "nccl":
+            try:
+                topo["rccl_version"] = ".".join(str(x) for x in torch.cuda.nccl.version())
+            except Exception:  # noqa: BLE001 -- informational only
+                pass
+        return topo
 
     def barrier(self):
         if self.world > 1:
             dist.barrier()
 
-    def max_over_ranks(self, x):
+    def _reduce(self, x, op):
         if self.world == 1:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=self.dev if self.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=op)
         return float(t.item())
 
+    def max_over_ranks(self, x):
+        return self._reduce(x, dist.ReduceOp.MAX if self.world > 1 else None)
+
     def sum_over_ranks(self, x):
+        return self._reduce(x, dist.ReduceOp.SUM if self.world > 1 else None)
+
+    def gather(self, obj):
+        """Every rank's `obj`, in rank order (on every rank)."""
         if self.world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64, device=self.dev if self.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return float(t.item())
+            return [obj]
+        out = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
 
 
 def timed_steps(ctx, step, steps, warmup):
@@ -127,6 +261,7 @@ def timed_steps(ctx, step, steps, warmup):
     lib.vbf_profile_enable(0)
     phases = profile_read()
     kms = [a.elapsed_time(b) for a, b in evs]
+    ctx.rank_wall = t1 - t0
     return ctx.max_over_ranks(t1 - t0), kms, phases
 
 
@@ -148,6 +283,37 @@ def phase_report(phases, steps):
     return {p: {"ms_per_launch": ms / n, "launches": n} for p, (ms, n) in phases.items() if n}
 
 
+def host_cpu_info():
+    """The host this rank runs on: model, the machine's logical CPUs, and the CPUs this process
+    may actually use (affinity mask and cgroup quota; on the GPU box a one-GPU lease is a share of
+    a larger machine)."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    logical = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = logical
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {"model": model, "logical_cpus": logical, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "usable_cores": usable}
+
+
 def cpu_baseline(keys_host, offsets_host, stride, n_sample, m, k, sample_desc, threads=1):
     """The oracle (a port of bf.rs:126-128 -> :84-92) on this node's host cores."""
     import oracle
@@ -163,11 +329,14 @@ def cpu_baseline(keys_host, offsets_host, stride, n_sample, m, k, sample_desc, t
 
 # ---------------------------------------------------------------------------------------
 def bench_fixed(ctx, args):
-    """Configs 2 / 4: fixed 16-byte keys, 10 bits per key, one filter per rank."""
-    n, L = args.keys, args.key_bytes
-    p = wl.fpr_for_bits_per_key(args.bits_per_key)
-    m, k = vbf.num_bits(n, p), vbf.num_hash_functions(vbf.num_bits(n, p), n)
-    seed = wl.SEED_CFG2 if ctx.world == 1 else wl.SEED_CFG4 + ctx.rank
+    """Configs 2 / 4: fixed 16-byte keys, 10 bits per key, one filter per rank.
+
+    Config 2 (the N=1 default): 100M keys, m = 1e9, seed 0x5EED0001.  Config 4 (the N>1 default):
+    rank r builds SSTable shard r -- 50M keys, m = 5e8, seed 0x5EED0040 + r -- as one merged
+    table's filter of a compaction (compactors/sized.rs:170-200, filter at :192-193)."""
+    L = args.key_bytes
+    w = rank_workload(args, ctx.rank)
+    n, m, k, seed = w["keys"], w["m"], w["k"], w["seed"]
     keys = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
     call("vbf_gen_fixed_dev", seed, 0, n, L, vp(keys), ctx.sp)
     nwords = (m + 31) // 32
@@ -184,6 +353,7 @@ def bench_fixed(ctx, args):
             evs.append((a, b))
 
     wall, kms, phases = timed_steps(ctx, step, args.steps, args.warmup)
+    rank_wall = ctx.rank_wall
 
     # post-timing checks on the last build: every key present; fill ratio
     cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
@@ -199,43 +369,61 @@ def bench_fixed(ctx, args):
     value = total_keys / wall
     kavg = float(np.mean(kms)) / 1e3
     bytes_per_key = L + m / (8.0 * n)
-    achieved = n * bytes_per_key / kavg / 1e9
+    ph = phase_report(phases, args.steps)
+    # the contract's roofline: algorithmic bytes of one build / the dominant kernel's mean launch
+    dom = max(ph, key=lambda q: ph[q]["ms_per_launch"] * ph[q]["launches"]) if ph else None
+    dom_s = ph[dom]["ms_per_launch"] / 1e3 if dom else kavg
+    achieved = n * bytes_per_key / dom_s / 1e9
     traffic, traffic_src = (pmc_traffic("traffic_config2.json") if (n, L, k) == (100_000_000, 16, 10)
                             and args.strategy != 1 else (None, None))
+    per_rank = ctx.gather({"rank": ctx.rank, "device": ctx.local, "keys": n, "seed": seed,
+                           "keys_per_s": n * args.steps / rank_wall, "ms_per_step": rank_wall / args.steps * 1e3,
+                           "fill_ratio": int(pop.item()) / m})
+    cfg_name = ("config4: %d independent SSTable shards x %dM x %dB keys, one per GPU (compaction fan-in), "
+                "%d bits/key (m=%d, k=%d per shard)" % (ctx.world, n // 10**6, L, args.bits_per_key, m, k)
+                if args.config == 4 else
+                "config2: %dM x %dB keys%s, %d bits/key (m=%d, k=%d)" % (
+                    n // 10**6, L, "" if ctx.world == 1 else " per GPU", args.bits_per_key, m, k))
     res = {
         "metric": "Bloom build keys/s (device-resident keys, bit-exact SipHash-1-3 filter)",
         "value": value, "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "key_gib_per_s": value * L / 2**30,
-        "config": {"workload": "config2: %dM x %dB keys per GPU, %d bits/key (m=%d, k=%d)%s" % (
-            n // 10**6, L, args.bits_per_key, m, k,
-            "" if ctx.world == 1 else
-            "; %d independent SSTable shards, one per GPU (config 4's compaction fan-in, weak scaling)" % ctx.world),
-            "n_keys_per_gpu": n, "key_bytes": L, "m_bits": m, "k": k, "len_prefix": True,
-            "parallelism": "independent shards x%d" % ctx.world},
+        "config": {"workload": cfg_name, "baseline_config": args.config,
+                   "n_keys_per_gpu": n, "key_bytes": L, "m_bits": m, "k": k, "len_prefix": True,
+                   "parallelism": "independent shards x%d" % ctx.world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "build (all phases of one vbf_build_dev_ex launch)", "kernel_ms": kavg * 1e3,
-                     "rocprof_kernels": {"tile_sort": "k_tile_pack<16, true, 10, true>", "transpose": "k_transpose_u16",
-                                         "seg_or": "k_seg_or<3, 1024, 5>"},
-                     "rocprof_summary": "profiles/r01/bench_default_kernel_stats.csv",
-                     "valu_frac_est": n * VALU_PER_KEY_CFG2 / kavg / VALU_PEAK_LANE_OPS,
+                     "kernel": dom, "kernel_ms": dom_s * 1e3,
+                     "build_ms": kavg * 1e3, "build_frac": n * bytes_per_key / kavg / 1e9 / HBM_PEAK_GBS,
+                     "rocprof_kernels": ROCPROF_KERNELS,
+                     "rocprof_summary": ROCPROF_SUMMARY,
+                     "valu_frac_est": (n * VALU_PER_KEY_CFG2 / dom_s / VALU_PEAK_LANE_OPS
+                                       if (L, k) == (16, 10) else None),
                      "algorithmic_bytes_per_key": bytes_per_key,
                      "siprounds_per_key": (L + 8) // 8 + 5 * k,
-                     "phases": phase_report(phases, args.steps)},
+                     "phases": ph},
         "fill_ratio": int(pop.item()) / m,
         "positive_sweep_ms": sweep,
+        "ranks": per_rank,
+        "topology": ctx.topology,
     }
     if ctx.world == 1 and ctx.rank == 0 and not args.no_cpu_baseline:
         ns = args.cpu_sample
         host = keys[: ns * L].cpu().numpy()
+        info = host_cpu_info()
+        res["host_cpu"] = info
         res["cpu_baseline"] = cpu_baseline(host, None, L, ns, m, k,
                                            "first %d of the %d keys, same m=%d/k=%d, 1 thread, ref-faithful "
                                            "(full SipHash per seed, u64 %%, serial like bf.rs:127)" % (ns, n, m, k))
-        if args.cpu_opt_threads:
-            t = args.cpu_opt_threads
-            res["cpu_opt"] = cpu_baseline(host, None, L, ns, m, k, "same sample, prefix-shared, %d threads" % t, threads=t)
+        t = args.cpu_opt_threads or info["usable_cores"]
+        if t:
+            res["cpu_opt"] = cpu_baseline(host, None, L, ns, m, k,
+                                          "same sample, prefix-shared hashing, %d threads = every core this process "
+                                          "may use (%s; %d logical CPUs on the machine)" % (
+                                              t, info["model"] or "unknown CPU", info["logical_cpus"]),
+                                          threads=t)
     return res
 
 
@@ -534,25 +722,43 @@ def bench_multi(ctx, args):
             "probes_per_s": ctx.sum_over_ranks(n) * S * args.steps / wall}
 
 
+def rank_workload(args, rank):
+    """(config, keys, m, k, seed) of `rank`'s build in the fixed-key configs (2 and 4)."""
+    n = args.keys or (100_000_000 if args.config == 2 else 50_000_000)
+    p = wl.fpr_for_bits_per_key(args.bits_per_key)
+    m = vbf.num_bits(n, p)
+    seed = (wl.SEED_CFG4 + rank) if args.config == 4 else (wl.SEED_CFG2 + 0x100 * rank)
+    return {"config": args.config, "keys": n, "m": m, "k": vbf.num_hash_functions(m, n), "seed": seed}
+
+
+def plan_only(args, world):
+    """The launch without the work: every rank joins the process group (gloo, CPU only) and
+    reports its workload; rank 0 prints them.  Tests the spawn path where there is no GPU."""
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == world
+    mine = dict(rank_workload(args, rank), rank=rank, local_rank=int(os.environ.get("LOCAL_RANK", "0")))
+    allr = [None] * world
+    if world > 1:
+        dist.all_gather_object(allr, mine)
+    else:
+        allr = [mine]
+    if rank == 0:
+        print(json.dumps({"plan_only": True, "world_size": world, "n_gpus": args.gpus, "ranks": allr}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--keys", type=int, default=None)
-    ap.add_argument("--key-bytes", type=int, default=16)
-    ap.add_argument("--bits-per-key", type=int, default=10)
-    ap.add_argument("--neg-keys", type=int, default=None)
-    ap.add_argument("--e2e", action="store_true")
-    ap.add_argument("--sst", action="store_true", help="SST data.db decode + rebuild (8(f) row 2)")
-    ap.add_argument("--compact", action="store_true", help="compaction merge + filter (8(f) row 3)")
-    ap.add_argument("--multi", action="store_true", help="batched multi-SST probe (8(f) row 4)")
-    ap.add_argument("--strategy", type=int, default=0, help="0 auto, 1 atomic, 2 partitioned")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=10_000_000)
-    ap.add_argument("--cpu-opt-threads", type=int, default=16)
-    args = ap.parse_args()
+    args = make_parser().parse_args()
+    mode, world = launch_plan(args.gpus, os.environ)
+    assert mode == "run", "maybe_spawn_ranks() handles --gpus N > 1 without a launcher"
+    args.gpus = world
+    if args.config is None:
+        args.config = 2 if world == 1 else 4
+    if args.plan_only:
+        return plan_only(args, world)
     ctx = Ctx(args)
     if args.config == 5:
         args.keys = args.keys or 1_000_000_000
@@ -574,6 +780,8 @@ def main():
     elif args.e2e:
         args.keys = args.keys or 100_000_000
         res = bench_e2e(ctx, args)
+    elif args.memtable:
+        res = bench_memtable(ctx, args)
     else:
         args.keys = args.keys or (100_000_000 if args.config == 2 else 50_000_000)
         res = bench_fixed(ctx, args)

@@ -55,6 +55,9 @@ extern "C" {
 #define VBF_ENODEV (-4)   /* no usable gfx950 device                                    */
 #define VBF_EDIVZERO (-5) /* m == 0 with k > 0: the reference panics (`% 0`, bf.rs:88)   */
 
+/* `device` of a filter whose bits live in host memory (see "Residency" below). */
+#define VBF_DEVICE_HOST (-1)
+
 const char* vbf_version(void);
 const char* vbf_last_error(void); /* thread-local; "" when the last call succeeded */
 int vbf_device_count(int* count);
@@ -163,18 +166,38 @@ typedef struct vbf_shard {
 } vbf_shard;
 int vbf_build_shards_host(vbf_shard* shards, uint64_t nshards, const int* devices, int ndevices);
 
-/* ---- BloomFilter handle: the bit array lives in HBM on `device` ---- */
+/* ---- BloomFilter handle: the bit array lives in HBM on `device` ----
+ *
+ * Residency.  A filter created on a device keeps its bits in that GPU's HBM: batch builds and
+ * probes run as kernels, and every call on the filter is ordered after the filter's previous
+ * one whatever stream either ran on (the reference's Mutex<BitVec>, bf.rs:85,96): a _dev call
+ * is queued behind the last asynchronous operation on the filter, a host call waits for it.
+ * A filter created with device = VBF_DEVICE_HOST keeps its bits in host memory and runs
+ * set/contains on the CPU inside this library (same SipHash-1-3 rounds, Rust's `hash % m`):
+ * the memtable's filter, one contains + set per put (memtable/mem.rs:207-221) and one contains
+ * per get (:223-230), where a kernel launch per key would cost two PCIe round trips.  Such a
+ * filter needs no GPU; the _dev, rebuild and multi-probe entry points reject it (VBF_EINVAL).
+ * vbf_filter_migrate moves a filter's bits between host and devices in place (clones follow).
+ *
+ * Element count.  no_of_elements (bf.rs:46) lives in the handle only: set_host / set_dev /
+ * rebuild add the number of keys, recover loads the stored n, clones copy it (bf.rs:248), and
+ * vbf_filter_set_num_elements assigns it (bf.rs:143).  A binding keeps no second counter. */
 typedef struct vbf_filter vbf_filter;
 
 int vbf_filter_new(double p, uint64_t no_of_elements, int device, vbf_filter** out); /* bf.rs:62-81 */
 int vbf_filter_default(int device, vbf_filter** out);                               /* bf.rs:256-267 */
+/* A filter of exactly m bits and k hash functions (the struct's pub fields set directly,
+ * bf.rs:38-58), no elements, false_positive_rate p. */
+int vbf_filter_new_sized(uint32_t m, uint32_t k, double p, int device, vbf_filter** out);
 /* recover_meta (bf.rs:135-150): k and n from the 16-byte metadata, m recomputed from n, bits 0. */
 int vbf_filter_recover(const uint8_t* meta, size_t len, int device, vbf_filter** out);
 int vbf_filter_clone(const vbf_filter* f, vbf_filter** out); /* shares the bit array, bf.rs:242-254 */
 void vbf_filter_free(vbf_filter* f);
 
 /* set over a batch (bf.rs:84-92 per key; build_filter_from_entries bf.rs:126-128).
- * no_of_elements += n (u32, wrapping like AtomicU32::fetch_add). */
+ * no_of_elements += n (u32, wrapping like AtomicU32::fetch_add).  _host takes host keys (any
+ * residency: a host-resident filter hashes them on the CPU, a device-resident one streams them
+ * to its GPU); _dev takes device keys and a stream (device-resident filters only). */
 int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets,
                         uint64_t stride, uint64_t n, int len_prefix);
 int vbf_filter_set_dev(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
@@ -189,8 +212,12 @@ uint32_t vbf_filter_num_bits(const vbf_filter* f);           /* bf.rs:204-207 */
 uint32_t vbf_filter_num_elements(const vbf_filter* f);       /* bf.rs:198-201 */
 uint32_t vbf_filter_num_hash_functions(const vbf_filter* f); /* bf.rs:210-213 */
 double vbf_filter_false_positive_rate(const vbf_filter* f);  /* bf.rs:54 */
-int vbf_filter_device(const vbf_filter* f);
-uint32_t* vbf_filter_words_dev(const vbf_filter* f); /* device pointer to the bit array */
+int vbf_filter_device(const vbf_filter* f);          /* a device id or VBF_DEVICE_HOST */
+uint32_t* vbf_filter_words_dev(const vbf_filter* f); /* device pointer to the bit array (NULL if host) */
+/* no_of_elements = n (bf.rs:143 assigns it on recover_meta). */
+int vbf_filter_set_num_elements(vbf_filter* f, uint32_t n);
+/* Move the (shared) bit array to `device` or to host memory (VBF_DEVICE_HOST), in place. */
+int vbf_filter_migrate(vbf_filter* f, int device);
 int vbf_filter_serialize(const vbf_filter* f, uint8_t out[16]); /* bf.rs:158-172 */
 /* clear (bf.rs:180-195): zero this filter's (shared) bits and return a fresh empty filter with
  * the same m, k and p. */
@@ -254,7 +281,10 @@ int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_
  * (src/key_range/range.rs:118,136).  Each key is hashed once for all filters.
  * filters: host array of handles, all on one device.  bounds / bounds_off (host): smallest_s =
  * bounds[bounds_off[2s] .. bounds_off[2s+1]), biggest_s = bounds[bounds_off[2s+1] ..
- * bounds_off[2s+2]).  A filter with m == 0 and k > 0 is VBF_EDIVZERO (bf.rs:100).
+ * bounds_off[2s+2]).  A key reaching a filter with m == 0 and k > 0 is VBF_EDIVZERO (bf.rs:100):
+ * without bounds every key reaches every filter, with bounds only the keys inside that SST's
+ * range do (one extra readback when such a filter is present).  Host-resident filters are
+ * rejected (vbf_filter_migrate them to the device first).
  * _dev: keys / offsets / out on that device, queued on `stream`.  _host: host buffers, synchronous. */
 int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                         int len_prefix, uint32_t nsst, const vbf_filter* const* filters,

@@ -42,6 +42,8 @@ for s in $STEPS; do
     compact) run bench_compact 600 python bench.py --compact --steps 5 --warmup 1 ;;
     multi)  run bench_multi 600 python bench.py --multi --steps 5 --warmup 1 ;;
     e2e)    run bench_e2e 600 python bench.py --e2e --steps 3 --warmup 1 ;;
+    dist2spawn) run bench_dist2_spawn 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    residency) run pytest_residency 600 python -u -m pytest tests/test_gpu_residency.py -x -v -m gpu --timeout 120 --timeout-method thread ;;
     dist2)  run bench_dist2 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;
     ubench) run ubench 300 ./tools/ubench ;;
     counters) (cd /tmp && run counters 120 rocprofv3 -L) || exit $? ;;

@@ -135,17 +135,22 @@ def test_filter_file_extension_roundtrip():
     import numpy as np
     from velarixdb_amd import filter_file
     w = np.arange(1, 1074, dtype=np.uint32) * np.uint32(2654435761)
-    raw = filter_file.encode(19, 1791, 1e-4, 34333, w)
+    raw = filter_file.encode(19, 1791, 1e-4, 34333, w, entries=2844)
     assert raw[:16] == struct.pack("<IId", 19, 1791, 1e-4)
-    k, n, p, m, words = filter_file.decode(raw)
-    assert (k, n, p, m) == (19, 1791, 1e-4, 34333) and np.array_equal(words, w)
+    k, n, p, m, words, ent = filter_file.decode(raw)
+    assert (k, n, p, m, ent) == (19, 1791, 1e-4, 34333, 2844) and np.array_equal(words, w)
+    assert filter_file.decode(filter_file.encode(19, 1791, 1e-4, 34333, w))[5] == 1791  # default: n
     # corrupted body -> ignored (caller rebuilds, as the reference does)
     bad = bytearray(raw)
     bad[-1] ^= 0xFF
-    assert filter_file.decode(bytes(bad))[3:] == (None, None)
+    assert filter_file.decode(bytes(bad))[3:] == (None, None, None)
+    # a version-1 extension (no entry count) is ignored too
+    v1 = bytearray(raw)
+    v1[20:24] = struct.pack("<I", 1)
+    assert filter_file.decode(bytes(v1))[3:] == (None, None, None)
     # the reference's own 16-byte files decode without words
     ref = open(os.path.join(ROOT, "tests/golden/sst_fixtures/sstable_1720785462309/filter.db"), "rb").read()
-    assert filter_file.decode(ref) == (19, 1791, 1e-4, None, None)
+    assert filter_file.decode(ref) == (19, 1791, 1e-4, None, None, None)
     with pytest.raises(EOFError):
         filter_file.decode(ref[:12])
 

@@ -16,6 +16,7 @@ VBF_EHIP = -2
 VBF_ENOMEM = -3
 VBF_ENODEV = -4
 VBF_EDIVZERO = -5
+VBF_DEVICE_HOST = -1
 
 VBF_BUILD_AUTO = 0
 VBF_BUILD_ATOMIC = 1
@@ -59,6 +60,7 @@ SIGNATURES = {
     "vbf_build_shards_host": (_int, [_vp, _u64, _vp, _int]),
     "vbf_filter_new": (_int, [_dbl, _u64, _int, ctypes.POINTER(_vp)]),
     "vbf_filter_default": (_int, [_int, ctypes.POINTER(_vp)]),
+    "vbf_filter_new_sized": (_int, [_u32, _u32, _dbl, _int, ctypes.POINTER(_vp)]),
     "vbf_filter_recover": (_int, [_vp, ctypes.c_size_t, _int, ctypes.POINTER(_vp)]),
     "vbf_filter_clone": (_int, [_vp, ctypes.POINTER(_vp)]),
     "vbf_filter_free": (None, [_vp]),
@@ -72,6 +74,8 @@ SIGNATURES = {
     "vbf_filter_false_positive_rate": (_dbl, [_vp]),
     "vbf_filter_device": (_int, [_vp]),
     "vbf_filter_words_dev": (_vp, [_vp]),
+    "vbf_filter_set_num_elements": (_int, [_vp, _u32]),
+    "vbf_filter_migrate": (_int, [_vp, _int]),
     "vbf_filter_serialize": (_int, [_vp, _vp]),
     "vbf_filter_clear": (_int, [_vp, ctypes.POINTER(_vp)]),
     "vbf_filter_words_to_host": (_int, [_vp, _vp, _u64]),

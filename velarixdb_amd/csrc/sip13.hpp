@@ -23,38 +23,44 @@ struct Sip {
 
 // 64-bit rotate by B < 32 as two v_alignbit_b32 (hipcc's own lowering of the C rotate is a
 // 64-bit shift + 32-bit shift + or: 22% slower for the whole hash, measured in tools/ubench).
+// The SipHash core below is also compiled for the host: the library's own single-key path for
+// host-resident (memtable) filters runs the same rounds on the CPU (vbf_api.hip).
 template <int B>
-__device__ __forceinline__ uint64_t rotl64(uint64_t x) {
+__host__ __device__ __forceinline__ uint64_t rotl64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
     const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - B);
     const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - B);
     return ((uint64_t)nhi << 32) | nlo;
+#else
+    return (x << B) | (x >> (64 - B));
+#endif
 }
 
 // Rotate by 32: swap the halves (free: register renaming).
-__device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x >> 32) | (x << 32); }
+__host__ __device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x >> 32) | (x << 32); }
 
-__device__ __forceinline__ void sip_round(Sip& s) {
+__host__ __device__ __forceinline__ void sip_round(Sip& s) {
     s.v0 += s.v1; s.v1 = rotl64<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap32(s.v0);
     s.v2 += s.v3; s.v3 = rotl64<16>(s.v3); s.v3 ^= s.v2;
     s.v0 += s.v3; s.v3 = rotl64<21>(s.v3); s.v3 ^= s.v0;
     s.v2 += s.v1; s.v1 = rotl64<17>(s.v1); s.v1 ^= s.v2; s.v2 = swap32(s.v2);
 }
 
-__device__ __forceinline__ Sip sip_init() {
+__host__ __device__ __forceinline__ Sip sip_init() {
     return Sip{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL,
                0x7465646279746573ULL};
 }
 
 // c = 1 compression round per 8-byte block.
-__device__ __forceinline__ void sip_compress(Sip& s, uint64_t m) {
+__host__ __device__ __forceinline__ void sip_compress(Sip& s, uint64_t m) {
     s.v3 ^= m;
     sip_round(s);
     s.v0 ^= m;
 }
 
 // Final block b (length byte << 56 | tail bytes) + d = 3 finalization rounds.
-__device__ __forceinline__ uint64_t sip_finish(Sip s, uint64_t b) {
+__host__ __device__ __forceinline__ uint64_t sip_finish(Sip s, uint64_t b) {
     s.v3 ^= b;
     sip_round(s);
     s.v0 ^= b;
@@ -76,7 +82,7 @@ struct Prefix {
 
 // Hash for seed i: one block (tail bytes || low bytes of LE64(i)), then the final block
 // (remaining seed bytes || length byte).  5 SipRounds per seed.
-__device__ __forceinline__ uint64_t prefix_hash(const Prefix& p, uint64_t seed) {
+__host__ __device__ __forceinline__ uint64_t prefix_hash(const Prefix& p, uint64_t seed) {
     Sip s = p.st;
     const uint32_t sb = p.r * 8;  // 0..56
     // sb == 0: block = seed, tail = 0.  The double shift keeps every shift count < 64.

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/vbf.h"
+#include "sip13.hpp"
 #include "vbf_kernels.hpp"
 
 namespace {
@@ -476,21 +477,126 @@ int pipeline_host_keys(Staging& st, const uint8_t* keys, const uint64_t* offsets
 // Filter handle.  Storage is shared between clones (bf.rs:249 clones the Arc).
 // ---------------------------------------------------------------------------------------
 struct Storage {
-    int device = 0;
+    int device = 0;  // VBF_DEVICE_HOST: the bits live in host memory (h_words), no HIP at all
     uint32_t m = 0;
     uint64_t nwords = 0;
     uint32_t* d_words = nullptr;
+    std::vector<uint32_t> h_words;
+    // The last asynchronous operation on d_words (a _dev call on the caller's stream): later
+    // calls on other streams wait for it on the device, host-side calls wait for it on the host,
+    // so every operation on one filter is ordered as the reference's Mutex<BitVec> orders them.
+    hipEvent_t last = nullptr;
+    bool pending = false;
     std::mutex mu;  // the reference's Mutex<BitVec>
+    bool host() const { return device == VBF_DEVICE_HOST; }
     ~Storage() {
         if (d_words) {
             int prev = -1;
             (void)hipGetDevice(&prev);
             (void)hipSetDevice(device);
+            if (pending) (void)hipEventSynchronize(last);
             (void)hipFree(d_words);
             if (prev >= 0) (void)hipSetDevice(prev);
         }
+        if (last) (void)hipEventDestroy(last);
     }
 };
+
+// Caller holds s.mu.  The stream `st` (any, including the legacy NULL stream) waits for the
+// filter's last asynchronous operation.
+int storage_wait(Storage& s, hipStream_t st) {
+    if (s.pending) HIP_TRY(hipStreamWaitEvent(st, s.last, 0));
+    return VBF_OK;
+}
+// Caller holds s.mu: the operation just queued on `st` is now the filter's last one.
+int storage_mark(Storage& s, hipStream_t st) {
+    if (!s.last) HIP_TRY(hipEventCreateWithFlags(&s.last, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(s.last, st));
+    s.pending = true;
+    return VBF_OK;
+}
+// Caller holds s.mu: the host waits until the filter's last asynchronous operation finished.
+int storage_sync(Storage& s) {
+    if (s.pending) {
+        HIP_TRY(hipEventSynchronize(s.last));
+        s.pending = false;
+    }
+    return VBF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Host-resident filters (VBF_DEVICE_HOST): the memtable's filter, built one key per put
+// (memtable/mem.rs:207-221: contains, then set) and probed one key per get (:223-230).  A GPU
+// launch per key would cost two PCIe round trips per put, so these run on the CPU in the
+// library, with the same SipHash-1-3 rounds as the kernels (sip13.hpp, compiled for the host)
+// and Rust's `hash % m` (bf.rs:88,99).
+// ---------------------------------------------------------------------------------------
+vbf::Prefix host_prefix(const uint8_t* key, uint64_t len, bool lp) {
+    vbf::Sip st = vbf::sip_init();
+    if (lp) vbf::sip_compress(st, len);  // Hash for [u8]: write_usize(len) first
+    uint64_t c = 0;
+    for (; c + 8 <= len; c += 8) {
+        uint64_t w;
+        std::memcpy(&w, key + c, 8);  // little-endian block
+        vbf::sip_compress(st, w);
+    }
+    vbf::Prefix p;
+    p.st = st;
+    p.r = (uint32_t)(len & 7);
+    uint64_t t = 0;
+    if (p.r) std::memcpy(&t, key + c, p.r);
+    p.tail = t;
+    p.total = (uint32_t)((len + (lp ? 8 : 0) + 8) & 0xff);
+    return p;
+}
+
+inline void host_key(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t j,
+                     const uint8_t** kp, uint64_t* len) {
+    if (offsets) {
+        *kp = keys + offsets[j];
+        *len = offsets[j + 1] - offsets[j];
+    } else {
+        *kp = keys + j * stride;
+        *len = stride;
+    }
+}
+
+// bf.rs:84-92 per key (the caller counts the elements).
+void host_set(Storage& s, uint32_t k, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+              uint64_t n, bool lp) {
+    uint32_t* w = s.h_words.data();
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint8_t* kp;
+        uint64_t len;
+        host_key(keys, offsets, stride, j, &kp, &len);
+        const vbf::Prefix p = host_prefix(kp, len, lp);
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t idx = (uint32_t)(vbf::prefix_hash(p, i) % (uint64_t)s.m);
+            w[idx >> 5] |= 1u << (idx & 31);
+        }
+    }
+}
+
+// bf.rs:95-105 per key: early exit on the first clear bit; k == 0 answers true.
+void host_contains(const Storage& s, uint32_t k, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                   uint64_t n, bool lp, uint8_t* out) {
+    const uint32_t* w = s.h_words.data();
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint8_t* kp;
+        uint64_t len;
+        host_key(keys, offsets, stride, j, &kp, &len);
+        const vbf::Prefix p = host_prefix(kp, len, lp);
+        uint8_t hit = 1;
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t idx = (uint32_t)(vbf::prefix_hash(p, i) % (uint64_t)s.m);
+            if (!((w[idx >> 5] >> (idx & 31)) & 1u)) {
+                hit = 0;
+                break;
+            }
+        }
+        out[j] = hit;
+    }
+}
 
 std::mutex g_stream_mu;
 std::vector<hipStream_t> g_filter_streams;
@@ -508,7 +614,9 @@ int new_storage(int device, uint32_t m, std::shared_ptr<Storage>* out) {
     s->device = device;
     s->m = m;
     s->nwords = ((uint64_t)m + 31) / 32;
-    if (s->nwords) {
+    if (device == VBF_DEVICE_HOST) {
+        s->h_words.assign(s->nwords, 0u);
+    } else if (s->nwords) {
         hipStream_t st;
         int rc = filter_stream(device, &st);
         if (rc) return rc;
@@ -967,18 +1075,28 @@ int vbf_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
 
 static int make_filter(int device, uint32_t m, uint32_t k, double p, vbf_filter** out) {
     if (!out) return fail(VBF_EINVAL, "out is NULL");
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
-        return fail(VBF_ENODEV, "no HIP device available");
-    if (device < 0 || device >= count) return fail(VBF_ENODEV, "device %d out of range (%d devices)", device, count);
-    DEVICE_SCOPE(device);
     std::unique_ptr<vbf_filter> f(new vbf_filter());
-    int rc = new_storage(device, m, &f->bits);
-    if (rc) return rc;
+    if (device == VBF_DEVICE_HOST) {
+        int rc = new_storage(device, m, &f->bits);
+        if (rc) return rc;
+    } else {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+            return fail(VBF_ENODEV, "no HIP device available");
+        if (device < 0 || device >= count)
+            return fail(VBF_ENODEV, "device %d out of range (%d devices)", device, count);
+        DEVICE_SCOPE(device);
+        int rc = new_storage(device, m, &f->bits);
+        if (rc) return rc;
+    }
     f->k = k;
     f->p = p;
     *out = f.release();
     return ok();
+}
+
+static int host_resident(const char* what) {
+    return fail(VBF_EINVAL, "%s: the filter is host-resident (VBF_DEVICE_HOST); use the _host entry points", what);
 }
 
 int vbf_filter_new(double p, uint64_t no_of_elements, int device, vbf_filter** out) {
@@ -989,6 +1107,10 @@ int vbf_filter_new(double p, uint64_t no_of_elements, int device, vbf_filter** o
 }
 
 int vbf_filter_default(int device, vbf_filter** out) { return make_filter(device, 0, 0, 0.0, out); }
+
+int vbf_filter_new_sized(uint32_t m, uint32_t k, double p, int device, vbf_filter** out) {
+    return make_filter(device, m, k, p, out);
+}
 
 int vbf_filter_recover(const uint8_t* meta, size_t len, int device, vbf_filter** out) {
     uint32_t k, n;
@@ -1007,7 +1129,7 @@ int vbf_filter_clone(const vbf_filter* f, vbf_filter** out) {
     vbf_filter* c = new vbf_filter();
     c->bits = f->bits;
     c->k = f->k;
-    c->n.store(f->n.load());
+    c->n.store(f->n.load());  // bf.rs:248: the clone's counter is a copy, the bits are shared
     c->p = f->p;
     *out = c;
     return ok();
@@ -1019,8 +1141,14 @@ uint32_t vbf_filter_num_bits(const vbf_filter* f) { return f ? f->bits->m : 0; }
 uint32_t vbf_filter_num_elements(const vbf_filter* f) { return f ? f->n.load() : 0; }
 uint32_t vbf_filter_num_hash_functions(const vbf_filter* f) { return f ? f->k : 0; }
 double vbf_filter_false_positive_rate(const vbf_filter* f) { return f ? f->p : 0.0; }
-int vbf_filter_device(const vbf_filter* f) { return f ? f->bits->device : -1; }
+int vbf_filter_device(const vbf_filter* f) { return f ? f->bits->device : VBF_DEVICE_HOST - 1; }
 uint32_t* vbf_filter_words_dev(const vbf_filter* f) { return f ? f->bits->d_words : nullptr; }
+
+int vbf_filter_set_num_elements(vbf_filter* f, uint32_t n) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    f->n.store(n);
+    return ok();
+}
 
 int vbf_filter_serialize(const vbf_filter* f, uint8_t out[16]) {
     if (!f || !out) return fail(VBF_EINVAL, "NULL argument");
@@ -1032,14 +1160,18 @@ int vbf_filter_set_dev(vbf_filter* f, const uint8_t* keys, const uint64_t* offse
                        uint64_t n, int len_prefix, void* stream) {
     if (!f) return fail(VBF_EINVAL, "filter is NULL");
     Storage& s = *f->bits;
+    if (s.host()) return host_resident("vbf_filter_set_dev");
     int rc = check_mk(s.m, f->k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
-    DEVICE_SCOPE(s.device);
-    {
+    if (n && f->k) {
+        DEVICE_SCOPE(s.device);
+        const hipStream_t hs = (hipStream_t)stream;
         std::lock_guard<std::mutex> lk(s.mu);
+        if ((rc = storage_wait(s, hs))) return rc;
         vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
-        if ((rc = do_build(kb, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, (hipStream_t)stream))) return rc;
+        if ((rc = do_build(kb, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, hs))) return rc;
+        if ((rc = storage_mark(s, hs))) return rc;
     }
     f->n.fetch_add((uint32_t)n);
     return ok();
@@ -1052,15 +1184,16 @@ int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offs
     int rc = check_mk(s.m, f->k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
-    if (n && f->k) {
+    if (n && f->k && s.host()) {
+        std::lock_guard<std::mutex> lk(s.mu);
+        host_set(s, f->k, keys, offsets, stride, n, len_prefix != 0);
+    } else if (n && f->k) {
         DEVICE_SCOPE(s.device);
         Staging* st = staging_for(s.device);
         std::lock_guard<std::mutex> lk(s.mu);
         std::lock_guard<std::mutex> lk2(st->mu);
         if ((rc = st->init(s.device))) return rc;
-        hipStream_t fs;
-        if ((rc = filter_stream(s.device, &fs))) return rc;
-        HIP_TRY(hipStreamSynchronize(fs));  // earlier async work on the filter stream
+        if ((rc = storage_sync(s))) return rc;  // earlier _dev work on this filter, any stream
         rc = pipeline_host_keys(
             *st, keys, offsets, stride, n, len_prefix, false,
             [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t hs) -> int {
@@ -1077,14 +1210,19 @@ int vbf_filter_contains_dev(const vbf_filter* f, const uint8_t* keys, const uint
                             uint64_t stride, uint64_t n, int len_prefix, uint8_t* out, void* stream) {
     if (!f) return fail(VBF_EINVAL, "filter is NULL");
     Storage& s = *f->bits;
+    if (s.host()) return host_resident("vbf_filter_contains_dev");
     int rc = check_mk(s.m, f->k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
     if (n && !out) return fail(VBF_EINVAL, "out is NULL");
+    if (n == 0) return ok();
     DEVICE_SCOPE(s.device);
+    const hipStream_t hs = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(s.mu);
+    if ((rc = storage_wait(s, hs))) return rc;
     vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
-    if ((rc = do_probe(kb, s.m, f->k, s.d_words, out, nullptr, VBF_BUILD_AUTO, (hipStream_t)stream))) return rc;
+    if ((rc = do_probe(kb, s.m, f->k, s.d_words, out, nullptr, VBF_BUILD_AUTO, hs))) return rc;
+    if ((rc = storage_mark(s, hs))) return rc;  // a later clear / load must not overtake the reads
     return ok();
 }
 
@@ -1097,14 +1235,17 @@ int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uin
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
     if (n && !out) return fail(VBF_EINVAL, "out is NULL");
     if (n == 0) return ok();
+    if (s.host()) {
+        std::lock_guard<std::mutex> lk(s.mu);
+        host_contains(s, f->k, keys, offsets, stride, n, len_prefix != 0, out);
+        return ok();
+    }
     DEVICE_SCOPE(s.device);
     Staging* st = staging_for(s.device);
     std::lock_guard<std::mutex> lk(s.mu);
     std::lock_guard<std::mutex> lk2(st->mu);
     if ((rc = st->init(s.device))) return rc;
-    hipStream_t fs;
-    if ((rc = filter_stream(s.device, &fs))) return rc;
-    HIP_TRY(hipStreamSynchronize(fs));
+    if ((rc = storage_sync(s))) return rc;
     rc = pipeline_host_keys(
         *st, keys, offsets, stride, n, len_prefix, true,
         [&](const vbf::KeyBatch& kb, uint64_t, int b, hipStream_t hs) -> int {
@@ -1123,14 +1264,19 @@ int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uin
 int vbf_filter_clear(vbf_filter* f, vbf_filter** out) {
     if (!f || !out) return fail(VBF_EINVAL, "NULL argument");
     Storage& s = *f->bits;
-    {
+    if (s.host()) {
+        std::lock_guard<std::mutex> lk(s.mu);
+        std::fill(s.h_words.begin(), s.h_words.end(), 0u);
+    } else {
         DEVICE_SCOPE(s.device);
         std::lock_guard<std::mutex> lk(s.mu);
         hipStream_t fs;
         int rc = filter_stream(s.device, &fs);
         if (rc) return rc;
+        if ((rc = storage_wait(s, fs))) return rc;  // a pending set_dev must not undo the clear
         if (s.nwords) HIP_TRY(hipMemsetAsync(s.d_words, 0, s.nwords * 4, fs));
         HIP_TRY(hipStreamSynchronize(fs));
+        s.pending = false;
     }
     return make_filter(s.device, s.m, f->k, f->p, out);
 }
@@ -1141,12 +1287,18 @@ int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords
     if (nwords < s.nwords || (s.nwords && !out)) return fail(VBF_EINVAL, "out holds %llu < %llu words",
                                                             (unsigned long long)nwords, (unsigned long long)s.nwords);
     if (!s.nwords) return ok();
+    if (s.host()) {
+        std::lock_guard<std::mutex> lk(s.mu);
+        std::memcpy(out, s.h_words.data(), s.nwords * 4);
+        return ok();
+    }
     DEVICE_SCOPE(s.device);
     std::lock_guard<std::mutex> lk(s.mu);
-    HIP_TRY(hipDeviceSynchronize());
+    int rc = storage_sync(s);  // this filter's pending work only: other filters keep running
+    if (rc) return rc;
     Staging* st = staging_for(s.device);
     std::lock_guard<std::mutex> lk2(st->mu);
-    int rc = st->init(s.device);
+    rc = st->init(s.device);
     if (!rc) rc = xfer_d2h(*st, out, s.d_words, s.nwords * 4);
     return rc ? rc : ok();
 }
@@ -1157,14 +1309,64 @@ int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nword
     if (nwords != s.nwords || (s.nwords && !in)) return fail(VBF_EINVAL, "expected %llu words, got %llu",
                                                             (unsigned long long)s.nwords, (unsigned long long)nwords);
     if (!s.nwords) return ok();
+    if (s.host()) {
+        std::lock_guard<std::mutex> lk(s.mu);
+        std::memcpy(s.h_words.data(), in, s.nwords * 4);
+        return ok();
+    }
     DEVICE_SCOPE(s.device);
     std::lock_guard<std::mutex> lk(s.mu);
-    HIP_TRY(hipDeviceSynchronize());
+    int rc = storage_sync(s);
+    if (rc) return rc;
     Staging* st = staging_for(s.device);
     std::lock_guard<std::mutex> lk2(st->mu);
-    int rc = st->init(s.device);
+    rc = st->init(s.device);
     if (!rc) rc = xfer_h2d(*st, s.d_words, in, s.nwords * 4);
     return rc ? rc : ok();
+}
+
+int vbf_filter_migrate(vbf_filter* f, int device) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    if (device != VBF_DEVICE_HOST) {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(VBF_ENODEV, "no HIP device available");
+        if (device < 0 || device >= count) return fail(VBF_ENODEV, "device %d out of range (%d devices)", device, count);
+    }
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (device == s.device) return ok();
+    std::vector<uint32_t> w;
+    if (s.host()) {
+        w.swap(s.h_words);
+    } else {
+        DEVICE_SCOPE(s.device);
+        int rc = storage_sync(s);
+        if (rc) return rc;
+        w.resize(s.nwords);
+        if (s.nwords) HIP_TRY(hipMemcpy(w.data(), s.d_words, s.nwords * 4, hipMemcpyDeviceToHost));
+    }
+    uint32_t* nd = nullptr;
+    if (device != VBF_DEVICE_HOST && s.nwords) {
+        DEVICE_SCOPE(device);
+        HIP_TRY(hipMalloc((void**)&nd, s.nwords * 4));
+        const hipError_t e = hipMemcpy(nd, w.data(), s.nwords * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            (void)hipFree(nd);
+            if (s.host()) s.h_words.swap(w);
+            return fail(VBF_EHIP, "hipMemcpy to device %d: %s", device, hipGetErrorString(e));
+        }
+    }
+    if (!s.host()) {  // release the old device copy (its work is finished: storage_sync above)
+        DEVICE_SCOPE(s.device);
+        if (s.d_words) HIP_TRY(hipFree(s.d_words));
+        if (s.last) (void)hipEventDestroy(s.last);
+        s.last = nullptr;
+        s.pending = false;
+    }
+    s.d_words = nd;
+    if (device == VBF_DEVICE_HOST) s.h_words.swap(w);
+    s.device = device;
+    return ok();
 }
 
 // ---- SST data.db decode ----
@@ -1255,6 +1457,7 @@ int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t
                                     uint64_t nblocks, uint64_t* n_out, void* stream) {
     if (!f) return fail(VBF_EINVAL, "filter is NULL");
     Storage& s = *f->bits;
+    if (s.host()) return host_resident("vbf_filter_rebuild_from_sst_dev");
     DEVICE_SCOPE(s.device);
     hipStream_t st = (hipStream_t)stream;
     uint64_t n = 0;
@@ -1275,8 +1478,10 @@ int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t
         const bool uniform = ulen != 0xFFFFFFFFu && ulen > 0;
         if ((rc = sst_emit_pass(a, d_keys, uniform ? nullptr : d_off, nullptr, nullptr, nullptr, st))) return rc;
         std::lock_guard<std::mutex> lk(s.mu);
+        if ((rc = storage_wait(s, st))) return rc;
         vbf::KeyBatch kb2 = uniform ? batch(d_keys, nullptr, 0, ulen, n, 1) : batch(d_keys, d_off, 0, 0, n, 1);
         if ((rc = do_build(kb2, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, st))) return rc;
+        if ((rc = storage_mark(s, st))) return rc;
     }
     f->n.fetch_add((uint32_t)n);
     return ok();
@@ -1286,6 +1491,7 @@ int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_
                                      uint64_t index_len, uint64_t* n_out) {
     if (!f || (len && !data) || (index_len && !index)) return fail(VBF_EINVAL, "NULL argument");
     Storage& s = *f->bits;
+    if (s.host()) return host_resident("vbf_filter_rebuild_from_sst_host");
     std::vector<uint32_t> blk;
     int rc = parse_index(index, index_len, &blk);
     if (rc) return rc;
@@ -1326,14 +1532,21 @@ int multi_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, u
                 uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds, const uint64_t* bounds_off,
                 uint8_t* out, hipStream_t s) {
     if (nsst && !filters) return fail(VBF_EINVAL, "filters is NULL");
+    bool zero_m = false;
     for (uint32_t i = 0; i < nsst; ++i) {
         if (!filters[i]) return fail(VBF_EINVAL, "filters[%u] is NULL", i);
+        if (filters[i]->bits->host()) return host_resident("vbf_multi_probe");
         if (filters[i]->bits->device != filters[0]->bits->device)
             return fail(VBF_EINVAL, "filters[%u] lives on device %d, filters[0] on %d", i, filters[i]->bits->device,
                         filters[0]->bits->device);
-        // bf.rs:100 divides by m: the reference panics once a key reaches such a filter
-        if (filters[i]->bits->m == 0 && filters[i]->k > 0 && n)
-            return fail(VBF_EDIVZERO, "filters[%u]: m == 0 with k = %u (bf.rs:100 divides by zero)", i, filters[i]->k);
+        // bf.rs:100 divides by m: the reference panics once a key reaches such a filter.  Without
+        // key ranges every key reaches every filter; with them only keys inside its range do.
+        if (filters[i]->bits->m == 0 && filters[i]->k > 0 && n) {
+            if (!bounds_off)
+                return fail(VBF_EDIVZERO, "filters[%u]: m == 0 with k = %u (bf.rs:100 divides by zero)", i,
+                            filters[i]->k);
+            zero_m = true;
+        }
     }
     if (bounds_off) {
         for (uint32_t i = 0; i < 2 * nsst; ++i)
@@ -1354,9 +1567,11 @@ int multi_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, u
     }
     const uint64_t nb = bounds_off ? bounds_off[2 * nsst] : 0;
     const uint64_t o_b = align256(nsst * sizeof(vbf::MultiSst));
+    const uint64_t o_err = o_b + align256(nb + 8);
     void* ws = nullptr;
-    int rc = get_workspace(s, o_b + nb + 8, &ws, kWsMulti);
+    int rc = get_workspace(s, o_err + 256, &ws, kWsMulti);
     if (rc) return rc;
+    uint32_t* d_err = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + o_err);
     // the table is read by this launch only; the stream orders reuse by the next call
     HIP_TRY(hipMemcpyAsync(ws, tab.data(), nsst * sizeof(vbf::MultiSst), hipMemcpyHostToDevice, s));
     uint8_t* d_bounds = nullptr;
@@ -1364,10 +1579,23 @@ int multi_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, u
         d_bounds = static_cast<uint8_t*>(ws) + o_b;
         if (nb) HIP_TRY(hipMemcpyAsync(d_bounds, bounds, nb, hipMemcpyHostToDevice, s));
     }
+    if (zero_m) HIP_TRY(hipMemsetAsync(d_err, 0, 4, s));
     HIP_TRY(hipStreamSynchronize(s));  // pageable sources: keep them alive only for this call
+    // every filter's pending work (set_dev on another stream) lands before the probe reads it
+    for (uint32_t i = 0; i < nsst; ++i)
+        if ((rc = storage_wait(*filters[i]->bits, s))) return rc;
     vbf::MultiArgs a{keys, offsets, 0, stride, n, nsst,
-                     static_cast<const vbf::MultiSst*>(ws), d_bounds, out};
+                     static_cast<const vbf::MultiSst*>(ws), d_bounds, out, d_err};
     HIP_TRY(vbf::launch_multi_probe(a, len_prefix != 0, s));
+    for (uint32_t i = 0; i < nsst; ++i)
+        if ((rc = storage_mark(*filters[i]->bits, s))) return rc;
+    if (zero_m) {  // rare (Default / p > 1 filters): one readback decides whether the reference panics
+        uint32_t e = 0;
+        HIP_TRY(hipMemcpyAsync(&e, d_err, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (e) return fail(VBF_EDIVZERO, "a key inside an SST's range reaches its filter with m == 0 < k "
+                                         "(bf.rs:100 divides by zero)");
+    }
     return VBF_OK;
 }
 }  // namespace
@@ -1380,6 +1608,7 @@ int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t s
     int rc = check_keys(keys, offsets, stride, n);
     if (rc) return rc;
     if (nsst && filters && filters[0]) {
+        if (filters[0]->bits->host()) return host_resident("vbf_multi_probe_dev");
         DEVICE_SCOPE(filters[0]->bits->device);
         MultiLock lk(filters, nsst);
         if ((rc = multi_probe(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out,
@@ -1405,6 +1634,7 @@ int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t 
     }
     if (!filters || !filters[0]) return fail(VBF_EINVAL, "filters is NULL");
     if (!out) return fail(VBF_EINVAL, "out is NULL");
+    if (filters[0]->bits->host()) return host_resident("vbf_multi_probe_host");
     DEVICE_SCOPE(filters[0]->bits->device);
     hipStream_t s;
     if ((rc = filter_stream(filters[0]->bits->device, &s))) return rc;

@@ -109,6 +109,7 @@ struct MultiArgs {
     const MultiSst* tab;    // device table, nsst entries
     const uint8_t* bounds;  // device, NULL = no key-range test
     uint8_t* out;           // n * nsst
+    uint32_t* err;          // device word: set to 1 when a key reaches a filter with m == 0 < k
 };
 hipError_t launch_multi_probe(const MultiArgs& a, bool len_prefix, hipStream_t s);
 // Compaction merge (vbf_compact.hip).

@@ -57,7 +57,10 @@ __global__ __launch_bounds__(256) void k_multi_probe(MultiArgs a) {
             hit = cmp_bytes(kp, kl, a.bounds + d.lo_beg, d.lo_end - d.lo_beg) >= 0 &&
                   cmp_bytes(kp, kl, a.bounds + d.hi_beg, d.hi_end - d.hi_beg) <= 0;
         }
-        if (hit && d.k > 0) {  // bf.rs:95-105, k == 0 -> true; early exit on the first clear bit
+        if (hit && d.k > 0 && d.m == 0) {  // bf.rs:100 `% 0`: the reference panics on this key
+            atomicOr(a.err, 1u);
+            hit = false;
+        } else if (hit && d.k > 0) {  // bf.rs:95-105, k == 0 -> true; early exit on the first clear bit
             if (!have) {
                 h0 = prefix_hash(p, 0);
                 h1 = prefix_hash(p, 1);

@@ -18,6 +18,10 @@ array resident in HBM.  Argument checks raise where the reference asserts or pan
 Batch forms (set_many / contains_many and the *_dev variants taking device pointers) are the
 accelerated entry points the compaction build (compactors/sized.rs:192-193), the lazy
 recovery rebuild (key_range/range.rs:117-128) and bulk probes use.
+
+Residency: `device` is a GPU index (bits in HBM, kernels) or HOST (bits in host memory, set /
+contains on the CPU inside libvbf with the kernels' SipHash rounds) -- the memtable's filter,
+one contains + set per put (memtable/mem.rs:207-221).  migrate() moves the bits in place.
 """
 import ctypes
 import os
@@ -25,11 +29,16 @@ import os
 import numpy as np
 
 from . import _lib, filter_file
-from ._lib import VBF_EDIVZERO, VBF_EINVAL, VbfError, call, lib
+from ._lib import VBF_DEVICE_HOST, VBF_EDIVZERO, VBF_EINVAL, VbfError, call, lib
 from .keys import HostBatch, encode, pack
 
 FILTER_FILE_NAME = "filter"  # consts/mod.rs:27
 DEFAULT_FALSE_POSITIVE_RATE = 1e-4  # consts/mod.rs:17
+HOST = VBF_DEVICE_HOST  # device= for a host-resident (memtable) filter
+
+
+def _dev(device):
+    return VBF_DEVICE_HOST if (device == "host" or device == HOST) else int(device)
 
 
 def num_bits(n, p):
@@ -59,12 +68,13 @@ class BloomFilter:
         self.sst_dir = None
         self.file_path = None
         self.bits_restored = False
+        self.restored_entries = None
         if _handle is not None:
             self._h = _handle
             return
         h = ctypes.c_void_p()
         try:
-            call("vbf_filter_new", float(false_positive_rate), int(no_of_elements), device, ctypes.byref(h))
+            call("vbf_filter_new", float(false_positive_rate), int(no_of_elements), _dev(device), ctypes.byref(h))
         except VbfError as e:
             _raise("new", e)
         self._h = h
@@ -73,7 +83,14 @@ class BloomFilter:
     @classmethod
     def default(cls, device=0):
         h = ctypes.c_void_p()
-        call("vbf_filter_default", device, ctypes.byref(h))
+        call("vbf_filter_default", _dev(device), ctypes.byref(h))
+        return cls(_handle=h)
+
+    @classmethod
+    def sized(cls, m, k, false_positive_rate=0.0, device=0):
+        """A filter of exactly m bits and k hash functions (the struct's pub fields set directly)."""
+        h = ctypes.c_void_p()
+        call("vbf_filter_new_sized", int(m), int(k), float(false_positive_rate), _dev(device), ctypes.byref(h))
         return cls(_handle=h)
 
     def clone(self):
@@ -107,6 +124,19 @@ class BloomFilter:
     @property
     def device(self):
         return int(lib.vbf_filter_device(self._h))
+
+    @property
+    def host_resident(self):
+        return self.device == VBF_DEVICE_HOST
+
+    def migrate(self, device):
+        """Move the (shared) bit array to GPU `device` or to host memory ("host"), in place."""
+        call("vbf_filter_migrate", self._h, _dev(device))
+        return self
+
+    def set_num_elements(self, n):
+        """bf.rs:143: `self.no_of_elements = AtomicU32::new(n)`."""
+        call("vbf_filter_set_num_elements", self._h, int(n) & 0xFFFFFFFF)
 
     def num_elements(self):
         return self.no_of_elements
@@ -212,11 +242,14 @@ class BloomFilter:
     def recover_from_sst_dir(self, sst_dir):
         """The lazy recovery of range.rs:117-128 for one SST directory: recover_meta() from its
         filter.db, then -- unless persisted bits were restored (filter_file.py) -- rebuild from
-        data.db + index.db.  Returns True when the bits came from filter.db."""
+        data.db + index.db.  Returns True when the bits came from filter.db.  Either way the
+        filter ends as the reference's recover_meta + build_filter_from_entries leaves it: the
+        same bits and no_of_elements = stored n + the SST's entries."""
         from . import sst
         self.file_path = os.path.join(os.fspath(sst_dir), FILTER_FILE_NAME + ".db")
         if self.recover_meta():
             self.sst_dir = os.fspath(sst_dir)
+            self.set_num_elements(self.no_of_elements + self.restored_entries)
             return True
         self.sst_dir = os.fspath(sst_dir)
         self.rebuild_from_sst(*sst.read_sst_files(sst_dir))
@@ -246,16 +279,18 @@ class BloomFilter:
         call("vbf_filter_serialize", self._h, buf)
         return bytes(buf)
 
-    def write(self, dir_path, persist_bits=True):
+    def write(self, dir_path, persist_bits=True, sst_entries=None):
         """bf.rs:114-123: write `filter.db` and remember its path.
 
         The first 16 bytes are exactly the reference's.  With persist_bits the bit array follows
-        (filter_file.py): invisible to the reference's reader, used by recover_meta() here."""
+        (filter_file.py): invisible to the reference's reader, used by recover_meta() here.
+        `sst_entries` is the SST's entry count (default no_of_elements, exact for a filter built
+        from its table's entries as compaction builds it)."""
         path = os.path.join(os.fspath(dir_path), FILTER_FILE_NAME + ".db")
         m = self.num_bits()
         words = self.words() if (persist_bits and m) else None
         raw = filter_file.encode(self.no_of_hash_func, self.no_of_elements, self.false_positive_rate,
-                                 m, words)
+                                 m, words, sst_entries)
         assert raw[:16] == self.serialize()
         with open(path, "wb") as f:
             f.write(raw)
@@ -274,7 +309,7 @@ class BloomFilter:
                 raw = f.read()
         except OSError:
             raise FileNotFoundError("Error opening filter file %s" % self.file_path) from None
-        k, n, p, m_saved, words = filter_file.decode(raw)
+        k, n, p, m_saved, words, entries = filter_file.decode(raw)
         meta = (ctypes.c_uint8 * 16).from_buffer_copy(raw[:16])
         h = ctypes.c_void_p()
         call("vbf_filter_recover", meta, 16, self.device, ctypes.byref(h))
@@ -282,6 +317,7 @@ class BloomFilter:
         self._h = h
         lib.vbf_filter_free(old)
         self.bits_restored = bool(load_bits and words is not None and m_saved == self.num_bits())
+        self.restored_entries = entries if self.bits_restored else None
         if self.bits_restored:
             self.load_words(words)
         return self.bits_restored

@@ -8,21 +8,26 @@ recomputed from the stored n (bf.rs:144-147).  Its reader consumes exactly 16 by
 here stays readable by the reference.
 
 Extension layout (little-endian), after the 16-byte header:
-    u32 magic 'VBFW' | u32 version (1) | u32 m | u32 nwords | u64 checksum(words) | words[nwords]
+    u32 magic 'VBFW' | u32 version (2) | u32 m | u32 nwords | u64 entries | u64 checksum(words)
+    | words[nwords]
+`entries` is the number of entries in the SST's data.db (what the reference's rebuild would
+add to no_of_elements, bf.rs:91 once per entry).
 
 On recovery the words are used only when the recorded m equals the m the reference would
 recompute (num_bits(n_stored, p)) -- then the loaded filter is bit-identical to the rebuild
-(same keys, same m, same k) and the rebuild can be skipped.  Otherwise (e.g. a memtable-born
-filter, sized from the write-buffer capacity) the caller rebuilds exactly as the reference does.
+(same keys, same m, same k) and the rebuild can be skipped; the element count becomes
+n_stored + entries, as recover_meta + build_filter_from_entries leave it (range.rs:121-124).
+Otherwise (e.g. a memtable-born filter, sized from the write-buffer capacity) the caller rebuilds
+exactly as the reference does.  Version-1 files (no entry count) are always rebuilt.
 """
 import struct
 
 import numpy as np
 
 HEADER = struct.Struct("<IId")
-EXT = struct.Struct("<IIIIQ")
+EXT = struct.Struct("<IIIIQQ")
 MAGIC = 0x57464256  # b"VBFW" little-endian
-VERSION = 1
+VERSION = 2
 
 
 def fast_checksum(words):
@@ -35,25 +40,29 @@ def fast_checksum(words):
         return int(np.bitwise_xor.reduce(w * np.uint64(0x9E3779B97F4A7C15) + idx * np.uint64(0xC2B2AE3D27D4EB4F)))
 
 
-def encode(k, n, p, m=None, words=None):
+def encode(k, n, p, m=None, words=None, entries=None):
+    """`entries`: the SST's data.db entry count (defaults to n, which is exact for a filter built
+    from its table's entries, as compaction builds them: sized.rs:192-193)."""
     out = HEADER.pack(k & 0xFFFFFFFF, n & 0xFFFFFFFF, p)
     if words is not None:
         w = np.ascontiguousarray(words, dtype="<u4")
-        out += EXT.pack(MAGIC, VERSION, m, w.size, fast_checksum(w)) + w.tobytes()
+        ent = n if entries is None else entries
+        out += EXT.pack(MAGIC, VERSION, m, w.size, ent, fast_checksum(w)) + w.tobytes()
     return out
 
 
 def decode(raw):
-    """-> (k, n, p, m_or_None, words_or_None); raises EOFError like FilterFileNode::recover."""
+    """-> (k, n, p, m_or_None, words_or_None, entries_or_None); raises EOFError like
+    FilterFileNode::recover."""
     if len(raw) < HEADER.size:
         raise EOFError("unexpected EOF: filter metadata is %d < 16 bytes" % len(raw))
     k, n, p = HEADER.unpack_from(raw, 0)
-    m = words = None
+    m = words = entries = None
     if len(raw) >= HEADER.size + EXT.size:
-        magic, ver, mm, nwords, chk = EXT.unpack_from(raw, HEADER.size)
+        magic, ver, mm, nwords, ent, chk = EXT.unpack_from(raw, HEADER.size)
         body = raw[HEADER.size + EXT.size:]
         if magic == MAGIC and ver == VERSION and len(body) == 4 * nwords and nwords == (mm + 31) // 32:
             w = np.frombuffer(body, dtype="<u4").astype(np.uint32)
             if fast_checksum(w) == chk:
-                m, words = mm, w
-    return k, n, p, m, words
+                m, words, entries = mm, w, ent
+    return k, n, p, m, words, entries
