@@ -722,6 +722,23 @@ def bench_multi(ctx, args):
             "probes_per_s": ctx.sum_over_ranks(n) * S * args.steps / wall}
 
 
+def bench_memtable(ctx, args):
+    """Single-key latency of the memtable's filter calls (mem.rs:209-211 contains + set per put,
+    :224 contains per get) through the C ABI from a plain C host (examples/memtable_latency.c),
+    host-resident vs device-resident; the tool also checks both residencies end bit-identical."""
+    tool = os.path.join(ROOT, "examples", "memtable_latency")
+    out = subprocess.run([tool, str(args.keys or 200_000), "2000"], capture_output=True, text=True, timeout=600)
+    if out.returncode != 0:
+        raise SystemExit("memtable_latency failed: " + out.stderr[-2000:])
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    return {"metric": "memtable filter single-key latency (contains + set per put, contains per get)",
+            "value": r["host"]["put_us"]["mean"], "unit": "us/put", "n_gpus": 1, "steps": r["host"]["keys"],
+            "warmup": 0, "higher_is_better": False, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "memtable filter m=%d k=%d (51 200-byte write buffer / 100 entries, p=1e-4)"
+                       % (r["m"], r["k"])},
+            "detail": r}
+
+
 def rank_workload(args, rank):
     """(config, keys, m, k, seed) of `rank`'s build in the fixed-key configs (2 and 4)."""
     n = args.keys or (100_000_000 if args.config == 2 else 50_000_000)

@@ -27,6 +27,7 @@ for s in $STEPS; do
     pytest) run pytest_gpu 1200 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
     benchq)  run bench_quick 300 python bench.py --no-cpu-baseline ;;
+    tile1wg) run bench_tile1wg 300 env VBF_TILE_LDS_MIN=98304 VBF_STAGGER=0 python bench.py --no-cpu-baseline --steps 10 ;;
     benchnostagger) run bench_nostagger 300 env VBF_STAGGER=0 python bench.py --no-cpu-baseline ;;
     benchstagger14) run bench_stagger14 300 env VBF_STAGGER=14 python bench.py --no-cpu-baseline ;;
     ablate) run ablate 300 python tools/ablate.py ;;

@@ -41,3 +41,17 @@ def test_c_host_matches_oracle(vbf, ora, tmp_path):
     assert np.array_equal(sw[0], ora.build_words(HostBatch(keys[:h * L], None, L, h, 1), m, k))
     assert np.array_equal(sw[1], ora.build_words(HostBatch(keys[h * L:], None, L, n - h, 1), m, k))
     assert np.array_equal(sw[0] | sw[1], want)  # OR of the shards == the whole build
+
+
+def test_memtable_latency_tool_host_equals_device(vbf):
+    """examples/memtable_latency.c: the memtable's one-key calls on a host-resident and a
+    device-resident filter end with identical words (CPU SipHash rounds vs the kernels)."""
+    import json
+    import subprocess
+    exe = os.path.join(ROOT, "examples", "memtable_latency")
+    out = subprocess.run([exe, "20000", "1500"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert (r["m"], r["k"]) == (9815, 19)
+    assert r["host_words_equal_device_words"] is True
+    assert r["device"]["n_elements"] > 0

@@ -237,10 +237,11 @@ def test_restored_bits_match_rebuild_count(vbf, tmp_path):
     assert np.array_equal(a.words(), b.words())
 
 
-def test_merged_table_filter_fpr(vbf, golden):
+def test_merged_table_filter_fpr(vbf, ora, golden):
     """sized_tier_test.rs:166-210: the 6-SST merge (17 064 entries) and its filter at the test
-    config's fpr 0.01: every merged key present, observed FPR within 1.1 x 0.01 (bf.rs's own
-    bound) on 20 000 keys no SST holds."""
+    config's fpr 0.01: every merged key present; on 20 000 keys no SST holds, the hits are the
+    oracle's exactly and the rate is the filter's fill^k.  (k = floor(m/n) = 9, not the optimal
+    m/n ln 2 = 6.6, so the rate is ~0.0114, above the configured 0.01: the reference's sizing.)"""
     from velarixdb_amd.compaction import CompactionConfig, SizedTierMerger
     tables = [vbf.sst.load_entries_from_dir(os.path.join(SST, n)) for n in NAMES[:6]]
     mg = SizedTierMerger(CompactionConfig(use_ttl=False, entry_ttl_ms=60_000, tombstone_ttl_ms=120_000,
@@ -252,8 +253,14 @@ def test_merged_table_filter_fpr(vbf, golden):
     assert bf.contains_many(keys).all()
     neg = [b"~neg%06d" % i for i in range(20000)]
     assert not set(neg) & set(keys)
-    fp = int(bf.contains_many(neg).sum())
-    assert fp / 20000 <= 0.01 * 1.1, fp
+    from velarixdb_amd.keys import pack
+    got = bf.contains_many(neg)
+    w = bf.words()
+    assert np.array_equal(got, ora.probe(pack(neg), bf.num_bits(), bf.no_of_hash_func, w).astype(bool))
+    fill = int(np.unpackbits(w.view(np.uint8)).sum()) / bf.num_bits()
+    expect = fill ** bf.no_of_hash_func
+    sigma = (expect * (1 - expect) / 20000) ** 0.5
+    assert abs(got.mean() - expect) < 5 * sigma, (got.mean(), expect)
 
 
 def test_multi_probe_zero_bit_filter_with_ranges(vbf):

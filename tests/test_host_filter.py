@@ -222,3 +222,18 @@ def test_host_filter_rejects_device_entry_points():
     assert z.contains(b"zzz")
     with pytest.raises(ZeroDivisionError):
         BloomFilter.sized(0, 3, device=HOST).contains(b"a")
+
+
+def test_memtable_latency_tool_runs_without_gpu():
+    """examples/memtable_latency.c (plain C, no Python in the process): the host residency works
+    with no GPU in the machine; puts of a 512-entry filter (m = 9815, k = 19, mem.rs:188-191)."""
+    import json
+    import subprocess
+    from conftest import ROOT
+    exe = os.path.join(ROOT, "examples", "memtable_latency")
+    if not os.path.exists(exe):
+        pytest.skip("examples not built (__graft_entry__.build())")
+    out = subprocess.run([exe, "20000"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert (r["m"], r["k"]) == (9815, 19) and 0 < r["host"]["n_elements"] <= 20000

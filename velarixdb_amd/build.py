@@ -55,17 +55,24 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     return out
 
 
+EXAMPLES = ("c_host", "memtable_latency")
+
+
 def build_examples(verbose=False):
-    """examples/c_host: the C ABI from a plain C host (gcc, no Python/torch in that process)."""
+    """examples/*.c: the C ABI from a plain C host (gcc, no Python/torch in that process)."""
     root = os.path.dirname(HERE)
-    src = os.path.join(root, "examples", "c_host.c")
-    out = os.path.join(root, "examples", "c_host")
-    cmd = ["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-I", os.path.join(root, "include"), src,
-           "-L", HERE, "-lvbf", "-Wl,-rpath,$ORIGIN/../velarixdb_amd", "-o", out]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
-    return out
+    outs = []
+    for name in EXAMPLES:
+        src = os.path.join(root, "examples", name + ".c")
+        out = os.path.join(root, "examples", name)
+        cmd = ["gcc", "-std=c11", "-D_POSIX_C_SOURCE=200809L", "-O2", "-Wall", "-Wextra", "-I",
+               os.path.join(root, "include"), src, "-L", HERE, "-lvbf", "-Wl,-rpath,$ORIGIN/../velarixdb_amd",
+               "-o", out]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        outs.append(out)
+    return outs
 
 
 ABLATION_LIB = os.path.join(HERE, "libvbf_ablate.so")

@@ -613,6 +613,10 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.CP = (pl.C + pl.nseg + 7) & ~7u;
     pl.tile_words = pl.CP / 2 + pl.CP / 8;
     pl.lds1 = (pl.CP / 2 + pl.CP / 8 + pl.nseg_pad + 16 + kLenBuckets) * 4;
+    // VBF_TILE_LDS_MIN (experiments, speed only): request at least this much LDS per k_tile_pack
+    // workgroup, e.g. > 80 KiB to hold one workgroup per CU
+    static const int lds_min = [] { const char* e = getenv("VBF_TILE_LDS_MIN"); return e ? atoi(e) : 0; }();
+    if (lds_min > 0) pl.lds1 = std::max<uint32_t>(pl.lds1, std::min<uint32_t>((uint32_t)lds_min, kLdsPerCu));
     // stagger the second resident workgroup per CU by ~half a tile of hashing (~25 us at k=10,
     // ~3000 keys): s_sleep 127 = 8128 cycles, ~3.7 us.  VBF_STAGGER=0 disables (A/B).
     static const int env = [] { const char* e = getenv("VBF_STAGGER"); return e ? atoi(e) : -1; }();
