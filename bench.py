@@ -41,6 +41,7 @@ def make_parser():
     ap.add_argument("--bits-per-key", type=int, default=10)
     ap.add_argument("--neg-keys", type=int, default=None)
     ap.add_argument("--e2e", action="store_true")
+    ap.add_argument("--e2e-fresh-out", action="store_true", help="--e2e: a fresh host array per step")
     ap.add_argument("--sst", action="store_true", help="SST data.db decode + rebuild (8(f) row 2)")
     ap.add_argument("--compact", action="store_true", help="compaction merge + filter (8(f) row 3)")
     ap.add_argument("--multi", action="store_true", help="batched multi-SST probe (8(f) row 4)")
@@ -548,7 +549,13 @@ def bench_cfg5(ctx, args):
 
 
 def bench_e2e(ctx, args):
-    """Keys in host memory (memtable / compaction output): vbf_filter_set_host end to end."""
+    """Keys in host memory (memtable / compaction output): vbf_filter_set_host end to end.
+
+    One step = BloomFilter::new (bf.rs:62-81, zeroed bits in HBM) + build_filter_from_entries over
+    the host keys (H2D in chunks overlapped with the kernels) + the finished words copied into
+    the caller's storage (the Rust BitVec the SST is written from).  The caller's storage is
+    allocated once and reused, as a long-lived writer's buffer would be; --e2e-fresh-out copies
+    into a fresh array every step (first-touch page faults included)."""
     n, L = args.keys, 16
     p = wl.fpr_for_bits_per_key(10)
     keys = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
@@ -557,21 +564,36 @@ def bench_e2e(ctx, args):
     del keys
     from velarixdb_amd.keys import HostBatch
     hb = HostBatch(host, None, L, n, 1)
-    times = []
+    out = None
+    times, phases = [], []
     for i in range(args.warmup + args.steps):
         t0 = time.perf_counter()
         bf = vbf.BloomFilter(p, n, device=ctx.local)
-        bf.set_batch(hb)
-        w = bf.words()  # D2H of the finished filter (written back with the SST)
         t1 = time.perf_counter()
+        bf.set_batch(hb)
+        t2 = time.perf_counter()
+        if out is None or args.e2e_fresh_out:
+            out = np.empty(bf.num_words(), dtype=np.uint32)
+            if not args.e2e_fresh_out:
+                out.fill(0)  # the caller's storage exists before the build (BitVec::from_elem)
+                t2 = time.perf_counter()
+        w = bf.words(out=out)  # D2H of the finished filter (written back with the SST)
+        t3 = time.perf_counter()
         if i >= args.warmup:
-            times.append(t1 - t0)
+            times.append(t3 - t0)
+            phases.append((t1 - t0, t2 - t1, t3 - t2))
         del bf
     t = float(np.median(times))
+    ph = np.median(np.array(phases), axis=0) * 1e3
+    link = (n * L + 4 * w.size) / 57e9  # measured pageable H2D/D2H rate of the box
     return {"metric": "Bloom build keys/s end-to-end (host keys: H2D + build + D2H)", "value": n / t,
             "unit": "keys/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": t * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u64", "data": "synthetic", "config": {"workload": "config2 e2e %dM x 16B, filter %d words" % (n // 10**6, w.size)}}
+            "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "config2 e2e %dM x 16B, filter %d words, %s output storage" % (
+                n // 10**6, w.size, "fresh" if args.e2e_fresh_out else "caller-owned, reused")},
+            "phases_ms": {"new": ph[0], "set_host_keys": ph[1], "words_to_host": ph[2]},
+            "link_floor_ms": link * 1e3}
 
 
 def bench_sst(ctx, args):

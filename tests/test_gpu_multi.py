@@ -106,3 +106,76 @@ def test_zero_bits_with_hashes_raises(vbf):
     with pytest.raises(ZeroDivisionError):
         contains_all([b"a"], [vbf.BloomFilter(0.01, 10), bad])
     assert contains_all([], [bad]).shape == (0, 1)
+
+
+@pytest.fixture
+def multi_mode():
+    """VBF_MULTI (read per call by libvbf): 1 = every filter one lane per key, 2 = interleaved
+    groups of equal-(m, k) filters whenever supported; restored afterwards."""
+    old = os.environ.get("VBF_MULTI")
+
+    def set_mode(v):
+        os.environ["VBF_MULTI"] = str(v)
+    yield set_mode
+    if old is None:
+        os.environ.pop("VBF_MULTI", None)
+    else:
+        os.environ["VBF_MULTI"] = old
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_interleaved_groups_match_oracle(vbf, ora, multi_mode, seed):
+    """Filters of one (m, k) probed as interleaved groups (vbf_multi_part.hip): groups of 3 and of
+    10 (split 8 + 2), mixed with filters of other sizes and an empty-range SST, with and without
+    key ranges; bit-exact against the oracle and against the one-lane-per-key path."""
+    from velarixdb_amd.key_range import SstRange, candidates, contains_all
+    rng = np.random.default_rng(seed)
+    specs = [(0.01, 4000)] * 3 + [(1e-4, 2500)] * 10 + [(0.05, 700), (0.001, 3000)]
+    order = rng.permutation(len(specs))
+    filters, orc, ranges = [], [], []
+    for i in order:
+        p, n = specs[i]
+        f = vbf.BloomFilter(p, n)
+        ks = sorted({rng.bytes(int(rng.integers(1, 24))) for _ in range(n)})
+        f.set_many(ks)
+        filters.append(f)
+        orc.append((f.num_bits(), f.no_of_hash_func, ora.build_words(vbf.pack(ks), f.num_bits(), f.no_of_hash_func)))
+        lo, hi = (ks[0], ks[-1]) if rng.random() < 0.8 else (b"\xff\xff", b"\xff\xff\x00")
+        ranges.append(SstRange(lo, hi, f))
+    q = [rng.bytes(int(rng.integers(0, 30))) for _ in range(30000)]
+    q += [r.smallest_key for r in ranges] + [r.biggest_key for r in ranges]
+    want_c = np.stack([_oracle_contains(ora, q, m, k, w) for m, k, w in orc], axis=1)
+    inr = np.array([[r.smallest_key <= x <= r.biggest_key for r in ranges] for x in q])
+    for mode in (2, 1):
+        multi_mode(mode)
+        assert np.array_equal(contains_all(q, filters), want_c), mode
+        assert np.array_equal(candidates(q, ranges), want_c & inr), mode
+
+
+def test_interleaved_groups_device_large(vbf, multi_mode):
+    """1.5M device keys x 8 same-size filters (the AUTO path): equals 8 single probes."""
+    import torch
+    from velarixdb_amd._lib import call
+    n, L, S = 1_500_000, 16, 8
+    dev = torch.device("cuda:0")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    keys = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    call("vbf_gen_fixed_dev", 0x5EED0C01, 0, n, L, P(keys), None)
+    filters = []
+    per = n // S
+    for s in range(S):
+        f = vbf.BloomFilter(0.0082, per)
+        f.set_dev(P(keys[s * per * L:]), None, L, per, 1)
+        filters.append(f)
+    handles = (ctypes.c_void_p * S)(*[f._h.value for f in filters])
+    multi_mode(0)
+    out = torch.empty(n * S, dtype=torch.uint8, device=dev)
+    call("vbf_multi_probe_dev", P(keys), None, L, n, 1, S, handles, None, None, P(out), None)
+    torch.cuda.synchronize()
+    got = out.view(n, S).cpu().numpy()
+    assert got.any(axis=1).all()  # every key is in one of the filters
+    for s, f in enumerate(filters):
+        one = torch.empty(n, dtype=torch.uint8, device=dev)
+        f.contains_dev(P(keys), None, L, n, P(one))
+        torch.cuda.synchronize()
+        assert np.array_equal(got[:, s], one.cpu().numpy()), s

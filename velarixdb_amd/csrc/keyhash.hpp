@@ -132,6 +132,16 @@ __device__ __forceinline__ Prefix key_prefix(const DevKeys& a, uint64_t j) {
     }
 }
 
+// Rust `Ord for [u8]`: lexicographic, a proper prefix is smaller.  -1 / 0 / 1.
+__device__ __forceinline__ int cmp_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
+    const uint64_t n = la < lb ? la : lb;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t x = a[i], y = b[i];
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
 // Host-side choice of FMT for a batch: the compile-time fixed layouts need aligned rows.
 enum KeyFmt { kFmtOffsets = -1, kFmtStride = 0 };
 

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <utility>
 #include <atomic>
 #include <cstdarg>
 #include <cstdlib>
@@ -112,6 +113,7 @@ enum WsSlot {
     kWsGather = 8,
     kWsProbe = 9,
     kWsCount = 10,
+    kWsMultiGroup = 11,
 };
 struct Workspace {
     int device;
@@ -150,6 +152,8 @@ int get_workspace(hipStream_t s, uint64_t bytes, void** out, int slot = kWsBuild
 }
 
 constexpr uint64_t kAutoPartitionMinIdx = 1ull << 22;
+// batched multi-SST probe: below this many keys every filter is probed one lane per key
+constexpr uint64_t kMultiGroupMinKeys = 1ull << 20;
 
 // The build every entry point funnels into.  strategy: VBF_BUILD_AUTO / _ATOMIC / _PARTITIONED.
 // atomic_merge: another writer may touch `words` concurrently (the partitioned path then
@@ -1555,15 +1559,55 @@ int multi_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, u
     }
     if (!n || !nsst) return VBF_OK;
     if (!out) return fail(VBF_EINVAL, "out is NULL");
-    std::vector<vbf::MultiSst> tab(nsst);
-    for (uint32_t i = 0; i < nsst; ++i) {
-        const Storage& st = *filters[i]->bits;
-        tab[i] = vbf::MultiSst{st.d_words, st.m, st.m ? ~0ull / st.m : 0, filters[i]->k, 0, 0, 0, 0, 0};
-        if (bounds_off) {
-            tab[i].lo_beg = bounds_off[2 * i];
-            tab[i].lo_end = tab[i].hi_beg = bounds_off[2 * i + 1];
-            tab[i].hi_end = bounds_off[2 * i + 2];
+    // Filters sharing (m, k) test the same positions for a key: interleave up to 8 of them and
+    // probe them together (vbf_multi_part.hip) when the batch is large; the rest one lane per key.
+    const char* menv = getenv("VBF_MULTI");  // A/B knob, read per call
+    const int mode = menv ? atoi(menv) : 0;
+    std::vector<vbf::MultiGroup> groups;
+    std::vector<char> grouped(nsst, 0);
+    if (mode != 1 && (mode == 2 || n >= kMultiGroupMinKeys)) {
+        std::vector<uint32_t> order(nsst);
+        for (uint32_t i = 0; i < nsst; ++i) order[i] = i;
+        auto key_of = [&](uint32_t i) { return std::make_pair(filters[i]->bits->m, filters[i]->k); };
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key_of(a) < key_of(b); });
+        for (uint32_t x = 0; x < nsst;) {
+            uint32_t y = x;
+            while (y < nsst && key_of(order[y]) == key_of(order[x])) ++y;
+            const uint32_t m = filters[order[x]]->bits->m, k = filters[order[x]]->k;
+            if (y - x >= 2 && vbf::multi_group_supported(m, k)) {
+                for (uint32_t a = x; a < y; a += vbf::kMaxGroup) {
+                    vbf::MultiGroup g{};
+                    g.m = m;
+                    g.k = k;
+                    g.G = std::min<uint32_t>(vbf::kMaxGroup, y - a);
+                    for (uint32_t q = 0; q < g.G; ++q) {
+                        const uint32_t i = order[a + q];
+                        g.words[q] = filters[i]->bits->d_words;
+                        g.col[q] = i;
+                        if (bounds_off) {
+                            g.lo_beg[q] = bounds_off[2 * i];
+                            g.lo_end[q] = g.hi_beg[q] = bounds_off[2 * i + 1];
+                            g.hi_end[q] = bounds_off[2 * i + 2];
+                        }
+                        grouped[i] = 1;
+                    }
+                    groups.push_back(g);
+                }
+            }
+            x = y;
         }
+    }
+    std::vector<vbf::MultiSst> tab;
+    for (uint32_t i = 0; i < nsst; ++i) {
+        if (grouped[i]) continue;
+        const Storage& st = *filters[i]->bits;
+        vbf::MultiSst e{st.d_words, st.m, st.m ? ~0ull / st.m : 0, filters[i]->k, i, 0, 0, 0, 0};
+        if (bounds_off) {
+            e.lo_beg = bounds_off[2 * i];
+            e.lo_end = e.hi_beg = bounds_off[2 * i + 1];
+            e.hi_end = bounds_off[2 * i + 2];
+        }
+        tab.push_back(e);
     }
     const uint64_t nb = bounds_off ? bounds_off[2 * nsst] : 0;
     const uint64_t o_b = align256(nsst * sizeof(vbf::MultiSst));
@@ -1573,7 +1617,8 @@ int multi_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, u
     if (rc) return rc;
     uint32_t* d_err = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + o_err);
     // the table is read by this launch only; the stream orders reuse by the next call
-    HIP_TRY(hipMemcpyAsync(ws, tab.data(), nsst * sizeof(vbf::MultiSst), hipMemcpyHostToDevice, s));
+    if (!tab.empty())
+        HIP_TRY(hipMemcpyAsync(ws, tab.data(), tab.size() * sizeof(vbf::MultiSst), hipMemcpyHostToDevice, s));
     uint8_t* d_bounds = nullptr;
     if (bounds_off) {
         d_bounds = static_cast<uint8_t*>(ws) + o_b;
@@ -1584,9 +1629,18 @@ int multi_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, u
     // every filter's pending work (set_dev on another stream) lands before the probe reads it
     for (uint32_t i = 0; i < nsst; ++i)
         if ((rc = storage_wait(*filters[i]->bits, s))) return rc;
-    vbf::MultiArgs a{keys, offsets, 0, stride, n, nsst,
-                     static_cast<const vbf::MultiSst*>(ws), d_bounds, out, d_err};
-    HIP_TRY(vbf::launch_multi_probe(a, len_prefix != 0, s));
+    const vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+    for (const vbf::MultiGroup& g : groups) {
+        const uint64_t need = vbf::multi_group_workspace_bytes(n, g.m, g.k);
+        void* gw = nullptr;
+        if ((rc = get_workspace(s, need, &gw, kWsMultiGroup))) return rc;
+        HIP_TRY(vbf::launch_multi_probe_group(kb, g, d_bounds, out, nsst, gw, need, s));
+    }
+    if (!tab.empty()) {
+        vbf::MultiArgs a{keys, offsets, 0, stride, n, (uint32_t)tab.size(),
+                         static_cast<const vbf::MultiSst*>(ws), d_bounds, out, d_err, nsst};
+        HIP_TRY(vbf::launch_multi_probe(a, len_prefix != 0, s));
+    }
     for (uint32_t i = 0; i < nsst; ++i)
         if ((rc = storage_mark(*filters[i]->bits, s))) return rc;
     if (zero_m) {  // rare (Default / p > 1 filters): one readback decides whether the reference panics

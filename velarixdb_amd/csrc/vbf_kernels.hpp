@@ -98,20 +98,35 @@ hipError_t sst_scan(const uint32_t* counts, uint64_t* ebase, uint64_t nblocks, v
 struct MultiSst {
     const uint32_t* words;
     uint64_t m, mu;
-    uint32_t k, pad;
+    uint32_t k, col;                          // col: the SST's column in `out`
     uint64_t lo_beg, lo_end, hi_beg, hi_end;  // smallest / biggest key in `bounds`
 };
 struct MultiArgs {
     const uint8_t* keys;
     const uint64_t* offsets;
     uint64_t off_base, stride, n;
-    uint32_t nsst;
+    uint32_t nsst;          // table entries
     const MultiSst* tab;    // device table, nsst entries
     const uint8_t* bounds;  // device, NULL = no key-range test
-    uint8_t* out;           // n * nsst
+    uint8_t* out;           // n rows of out_stride bytes
     uint32_t* err;          // device word: set to 1 when a key reaches a filter with m == 0 < k
+    uint32_t out_stride;    // all SSTs of the call
 };
 hipError_t launch_multi_probe(const MultiArgs& a, bool len_prefix, hipStream_t s);
+// Interleaved groups (vbf_multi_part.hip): G <= 8 filters of one (m, k) probed together, their bits
+// interleaved into one byte per position; a partitioned probe tests all G per entry.
+constexpr uint32_t kMaxGroup = 8;
+struct MultiGroup {
+    const uint32_t* words[kMaxGroup];
+    uint32_t G, k;
+    uint64_t m;
+    uint32_t col[kMaxGroup];
+    uint64_t lo_beg[kMaxGroup], lo_end[kMaxGroup], hi_beg[kMaxGroup], hi_end[kMaxGroup];
+};
+bool multi_group_supported(uint64_t m, uint32_t k);
+uint64_t multi_group_workspace_bytes(uint64_t n, uint64_t m, uint32_t k);
+hipError_t launch_multi_probe_group(const KeyBatch& kb, const MultiGroup& g, const uint8_t* bounds, uint8_t* out,
+                                    uint32_t out_stride, void* ws, uint64_t ws_bytes, hipStream_t s);
 // Compaction merge (vbf_compact.hip).
 struct CompactArgs {
     const uint8_t* keys;

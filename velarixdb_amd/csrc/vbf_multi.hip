@@ -19,16 +19,6 @@
 
 namespace vbf {
 
-// Rust `Ord for [u8]`: lexicographic, a proper prefix is smaller.  -1 / 0 / 1.
-__device__ __forceinline__ int cmp_bytes(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
-    const uint64_t n = la < lb ? la : lb;
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint32_t x = a[i], y = b[i];
-        if (x != y) return x < y ? -1 : 1;
-    }
-    return la < lb ? -1 : (la > lb ? 1 : 0);
-}
-
 template <int FMT, bool LP>
 __global__ __launch_bounds__(256) void k_multi_probe(MultiArgs a) {
     const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -49,7 +39,7 @@ __global__ __launch_bounds__(256) void k_multi_probe(MultiArgs a) {
     // array (a scratch load per bit test).
     uint64_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
     bool have = false;
-    uint8_t* out = a.out + j * a.nsst;
+    uint8_t* out = a.out + j * a.out_stride;
     for (uint32_t s = 0; s < a.nsst; ++s) {
         const MultiSst d = a.tab[s];
         bool hit = true;
@@ -75,7 +65,7 @@ __global__ __launch_bounds__(256) void k_multi_probe(MultiArgs a) {
             hit = test(h0) && (d.k < 2 || test(h1)) && (d.k < 3 || test(h2)) && (d.k < 4 || test(h3));
             for (uint32_t i = 4; hit && i < d.k; ++i) hit = test(prefix_hash(p, i));
         }
-        out[s] = hit ? 1 : 0;
+        out[d.col] = hit ? 1 : 0;
     }
 }
 

@@ -78,4 +78,17 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
 // K2 (vbf_partition.hip): ends[rows][cols] -> endsT[cols][rows], shared by build and probe.
 void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t s);
 
+// Partitioned probe plan (vbf_probe_part.hip): KT keys per tile, C = KT * k entries, segments of
+// 2^sb filter positions, `cap` padded entries per tile in the workspace.
+struct ProbePlan {
+    uint32_t k, R, KT, C, nseg, nseg_pad, cap, lds1;
+    uint64_t m, mu, nwords;
+};
+// Segments of an interleaved group of filters (vbf_multi_part.hip): 2^17 one-byte positions.
+constexpr int kByteSegBits = 17;
+ProbePlan make_probe_plan(uint32_t m, uint32_t k, int sb);
+// Q1 (hash + sort entries by segment) for segments of 2^sb positions (kSegBits or kByteSegBits).
+hipError_t launch_probe_pack(const KeyBatch& kb, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
+                             uint32_t* tiles, uint16_t* ends, int sb, hipStream_t s);
+
 }  // namespace vbf

@@ -17,16 +17,14 @@ namespace vbf {
 //                     the answer byte (or count the hits).
 // Without early exit every key costs k hashes, but no probe leaves the chip's LDS.
 // =================================================================================================
-struct ProbePlan {
-    uint32_t k, R, KT, C, nseg, nseg_pad, cap, lds1;
-    uint64_t m, mu, nwords;
-};
-
 constexpr uint32_t kOffMask = (1u << kSegBits) - 1;
 static_assert(kSegBits == 20, "probe entries hold a 12-bit key id above the 20-bit offset");
 
-template <int FMT, bool LP, int K, bool M31>
+// SB: segment = 2^SB filter positions (bits of one filter: 20; bytes of an interleaved group of
+// filters, vbf_multi_part.hip: 17).  An entry is (tile-local key id << SB) | offset in segment.
+template <int FMT, bool LP, int K, bool M31, int SB>
 __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan pl, uint32_t* tiles, uint16_t* ends) {
+    constexpr uint32_t kOff = (1u << SB) - 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* ent = smem;               // C entries
     uint32_t* cnt = ent + pl.C;         // nseg_pad: counts -> starts -> ends
@@ -53,7 +51,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
-                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    atomicAdd(&cnt[idx >> SB], 1u);
                 }
                 stash[r * K + i] = idx;
             }
@@ -73,7 +71,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
-                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    atomicAdd(&cnt[idx >> SB], 1u);
                 }
                 stash[ns++] = idx;
             }
@@ -96,13 +94,13 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> kSegBits], 1u) : 0u;
+            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> SB], 1u) : 0u;
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q)
             if (val[q] != kSentinel) {
                 const uint32_t local = ((t + q) / per) * kPBlock + tid;  // round r = slot / k
-                ent[pos[q]] = (local << kSegBits) | (val[q] & kOffMask);
+                ent[pos[q]] = (local << SB) | (val[q] & kOff);
             }
     }
     __syncthreads();
@@ -290,13 +288,13 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out(const uint32_t* tiles, co
     }
 }
 
-static ProbePlan make_probe_plan(uint32_t m, uint32_t k) {
+ProbePlan make_probe_plan(uint32_t m, uint32_t k, int sb) {
     ProbePlan pl{};
     pl.k = k;
     pl.m = m;
     pl.mu = ~0ull / m;
     pl.nwords = ((uint64_t)m + 31) / 32;
-    pl.nseg = (uint32_t)(((uint64_t)m + (1u << kSegBits) - 1) >> kSegBits);
+    pl.nseg = (uint32_t)(((uint64_t)m + (1u << sb) - 1) >> sb);
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
     const uint32_t rmax = (uint32_t)rounds_max((int)k);
     const int64_t avail = (int64_t)(kLdsPerCu / 2) - 64 - 8 * (int64_t)pl.nseg_pad;
@@ -311,7 +309,7 @@ static ProbePlan make_probe_plan(uint32_t m, uint32_t k) {
 
 bool probe_partition_supported(uint32_t m, uint32_t k) {
     if (m == 0 || k < 1 || k > (uint32_t)kStash) return false;
-    const ProbePlan pl = make_probe_plan(m, k);
+    const ProbePlan pl = make_probe_plan(m, k, kSegBits);
     return pl.KT >= 64 && pl.lds1 <= kLdsPerCu / 2 && pl.cap <= 65535;
 }
 
@@ -322,21 +320,50 @@ static uint64_t probe_chunk_keys(const ProbePlan& pl, uint64_t n) {
 
 uint64_t probe_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     if (!probe_partition_supported(m, k)) return 0;
-    const ProbePlan pl = make_probe_plan(m, k);
+    const ProbePlan pl = make_probe_plan(m, k, kSegBits);
     const uint64_t ntiles = (probe_chunk_keys(pl, n) + pl.KT - 1) / pl.KT;
     return ntiles * ((uint64_t)pl.cap * 4 + pl.cap / 8 + (uint64_t)pl.nseg * 4 + 4) + 1024;
 }
 
 uint64_t probe_count_partials(uint64_t n, uint32_t m, uint32_t k) {
-    const ProbePlan pl = make_probe_plan(m, k);
+    const ProbePlan pl = make_probe_plan(m, k, kSegBits);
     return (probe_chunk_keys(pl, n) + pl.KT - 1) / pl.KT;
+}
+
+template <int FMT, bool LP, int SB>
+hipError_t launch_probe_pack_fmt(const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles, uint32_t* tiles,
+                                 uint16_t* ends, hipStream_t s) {
+    const uint32_t k = pl.k;
+    auto pick = [&]<bool S>() {
+        return k == 10 ? k_probe_pack<FMT, LP, 10, S, SB>
+             : k == 4  ? k_probe_pack<FMT, LP, 4, S, SB>
+             : k == 19 ? k_probe_pack<FMT, LP, 19, S, SB>  // the reference's default p = 1e-4
+                       : k_probe_pack<FMT, LP, 0, false, SB>;
+    };
+    auto fn = pl.m <= (1ull << 31) ? pick.template operator()<true>() : pick.template operator()<false>();
+    hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)pl.lds1);
+    if (err == hipSuccess) hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
+    return err;
+}
+
+hipError_t launch_probe_pack(const KeyBatch& kb, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
+                             uint32_t* tiles, uint16_t* ends, int sb, hipStream_t s) {
+    hipError_t err = hipErrorInvalidValue;
+    with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
+        if (sb == kSegBits)
+            err = launch_probe_pack_fmt<FMT, LP, kSegBits>(dk, pl, ntiles, tiles, ends, s);
+        else if (sb == kByteSegBits)
+            err = launch_probe_pack_fmt<FMT, LP, kByteSegBits>(dk, pl, ntiles, tiles, ends, s);
+    });
+    return err;
 }
 
 hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
                                     unsigned long long* count, void* ws, uint64_t ws_bytes, hipStream_t s) {
     if (kb.n == 0) return hipSuccess;
     if (!probe_partition_supported(m, k)) return hipErrorInvalidValue;
-    const ProbePlan pl = make_probe_plan(m, k);
+    const ProbePlan pl = make_probe_plan(m, k, kSegBits);
     const uint64_t chunk_keys = probe_chunk_keys(pl, kb.n);
     const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
     if (ws_bytes < probe_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;
@@ -362,17 +389,7 @@ hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         hipError_t err = hipSuccess;
         phase_begin(kPhaseProbePack, s);
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
-            auto pick = [&]<bool S>() {
-                return k == 10 ? k_probe_pack<FMT, LP, 10, S>
-                     : k == 4  ? k_probe_pack<FMT, LP, 4, S>
-                     : k == 19 ? k_probe_pack<FMT, LP, 19, S>  // the reference's default p = 1e-4
-                               : k_probe_pack<FMT, LP, 0, false>;
-            };
-            auto fn = m <= (1u << 31) ? pick.template operator()<true>() : pick.template operator()<false>();
-            err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
-            if (err == hipSuccess)
-                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
+            err = launch_probe_pack_fmt<FMT, LP, kSegBits>(dk, pl, ntiles, tiles, ends, s);
         });
         if (err != hipSuccess) return err;
         launch_transpose_u16(ends, endsT, ntiles, pl.nseg, s);

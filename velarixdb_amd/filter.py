@@ -256,9 +256,17 @@ class BloomFilter:
         return False
 
     # -- bits ----------------------------------------------------------------------------
-    def words(self):
-        """The bit array as uint32 words (bit-vec BitVec<u32> storage)."""
-        w = np.zeros(self.num_words(), dtype=np.uint32)
+    def words(self, out=None):
+        """The bit array as uint32 words (bit-vec BitVec<u32> storage).  `out`: caller-owned
+        storage to copy into (a uint32 array of at least num_words(); the Rust caller's BitVec
+        storage), e.g. one already written once so its pages are resident."""
+        n = self.num_words()
+        if out is None:
+            w = np.zeros(n, dtype=np.uint32)
+        else:
+            w = out
+            if w.dtype != np.uint32 or not w.flags.c_contiguous or w.size < n:
+                raise ValueError("out must be a contiguous uint32 array of >= %d words" % n)
         call("vbf_filter_words_to_host", self._h, w.ctypes.data if w.size else None, w.size)
         return w
 
