@@ -119,6 +119,9 @@ def test_hashes_variable_length_unaligned(vbf, ora):
                                       (32, 1, 4_000_003, 4), (24, 1, 777_777, 7), (12, 1, 50_000, 5),
                                       (16, 0, 65536, 32), (100, 1, 1_000_003, 2),
                                       (16, 1, 3_000_000_017, 1), (16, 1, 4294967295, 4),
+                                      # k = 19 (p = 1e-4): two lanes per key for fixed layouts
+                                      (16, 1, 3_800_017, 19), (32, 0, 500_009, 19), (24, 1, 2_000_003, 19),
+                                      (16, 1, 2_999_999_999, 19),
                                       # either side of m = 2^31, where the build switches remainder code
                                       (16, 1, 2147483648, 10), (16, 1, 2147483649, 10), (16, 1, 2147483647, 4)])
 def test_build_fixed_matches_oracle(vbf, ora, L, lp, m, k, strategy):

@@ -75,6 +75,31 @@ def test_config2_full_size_bit_exact(vbf, ora):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.timeout(600)
+def test_k19_full_size_bit_exact(vbf, ora):
+    """The reference's default p = 1e-4 gives k = 19 (consts/mod.rs:17, bf.rs:236-239): config 2's
+    100M keys at 19 bits per key (m = 1.9e9), built with two lanes per key (vbf_partition.hpp
+    build_spl), bit-exact against the atomic build and the 16-thread oracle over all 100M keys."""
+    from velarixdb_amd.keys import HostBatch
+    from velarixdb_amd.workloads import SEED_CFG2, fpr_for_bits_per_key
+    n, L = 100_000_000, 16
+    m = vbf.num_bits(n, fpr_for_bits_per_key(19))
+    k = vbf.num_hash_functions(m, n)
+    assert (m, k) == (1_900_000_000, 19)
+    keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG2, 0, n, L, vp(keys), sp())
+    w_part = build(vbf, keys, None, L, n, m, k, 2)
+    w_atom = build(vbf, keys, None, L, n, m, k, 1)
+    assert torch.equal(w_part, w_atom)
+    assert count(vbf, keys, None, L, n, m, k, w_part) == n
+    fill = popcount(vbf, w_part) / m
+    assert abs(fill - (1 - math.exp(-k * n / m))) < 1e-3
+    host = keys.cpu().numpy()
+    del keys, w_atom
+    want = ora.build_words(HostBatch(host, None, L, n, 1), m, k, threads=16)
+    assert np.array_equal(w_part.cpu().numpy().view(np.uint32), want)
+
+
 def test_config3_full_size_properties(vbf, ora):
     from velarixdb_amd.keys import pack_offsets
     from velarixdb_amd.workloads import SEED_CFG3, SEED_CFG3_NEG, fpr_for_bits_per_key, var_offsets

@@ -110,7 +110,13 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     if (FMT < 0 && tid < kLenBuckets) lhist[tid] = 0;
     __syncthreads();
 
-    uint32_t stash[K > 0 ? build_rounds_max(K) * K : kStash];
+    // SPL lanes per key (build_spl): lane tid takes key slot r * (kPBlock / SPL) + tid / SPL and
+    // seeds [KL * (tid % SPL), KL * (tid % SPL) + KL) of it
+    constexpr int SPL = K > 0 ? build_spl(K, FMT > 0) : 1;
+    constexpr int KL = K > 0 ? build_kl(K, FMT > 0) : 1;
+    constexpr uint32_t kKeysPerRound = kPBlock / SPL;
+    constexpr int RMK = K > 0 ? build_rounds_max(K, FMT > 0) : 1;
+    uint32_t stash[K > 0 ? RMK * KL : kStash];
     const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
     const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
     const uint32_t nk = (uint32_t)(key_end - key0);
@@ -136,14 +142,15 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     auto key_of = [&](uint32_t slot) -> uint64_t { return key0 + (perm ? (uint32_t)lo[slot] : slot); };
     uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
     if constexpr (K > 0) {
-        constexpr int RM = build_rounds_max(K);
+        constexpr int RM = RMK;
         // One instance per round with r a compile-time constant: the stash index r*K+i stays
         // static even where the round body holds a runtime loop (the offsets layout's absorb),
         // which keeps LLVM from unrolling a plain `for` -- the stash then went to scratch
         // memory (128 B per lane of scratch stores and loads per key, variable-length builds).
         auto round = [&](auto rc) {
             constexpr int r = decltype(rc)::value;
-            const uint32_t slot = (uint32_t)r * kPBlock + tid;
+            const uint32_t slot = (uint32_t)r * kKeysPerRound + tid / SPL;
+            const uint32_t seed0 = (uint32_t)KL * (tid % SPL);
             const bool valid = (uint32_t)r < pl.R && slot < nk;
             Prefix p{};
             if (valid) {
@@ -163,19 +170,19 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
                 }
             }
 #pragma unroll
-            for (int i = 0; i < K; ++i) {
+            for (int i = 0; i < KL; ++i) {
                 uint32_t idx = kSentinel;
-                if (valid) {
-                    idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
+                if (valid && (SPL == 1 || seed0 + i < (uint32_t)K)) {
+                    idx = mod_m<M31>(prefix_hash(p, seed0 + i), pl.m, pl.mu);
                     atomicAdd(&cnt[idx >> kSegBits], 1u);
                 }
-                stash[r * K + i] = idx;
+                stash[r * KL + i] = idx;
             }
         };
         [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
             (round(std::integral_constant<int, Rs>{}), ...);
         }(std::make_integer_sequence<int, RM>{});
-        ns = RM * K;
+        ns = RM * KL;
     } else {
         ns = 0;
         for (uint32_t r = 0; r < pl.R; ++r) {
@@ -206,7 +213,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     }
     // rank + place, 8 returning LDS atomics in flight before their results are used
     // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
-    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(build_rounds_max(K) * K) : (uint32_t)kStash;
+    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(RMK * KL) : (uint32_t)kStash;
 #pragma unroll
     for (uint32_t t = 0; t < kNsMax; t += 8) {
         if (t >= ns) break;
@@ -586,7 +593,9 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
 
 // Tile size: the largest KT (<= kStash/k rounds of 1024 keys) whose packed LDS image fits two
 // workgroups per CU; one per CU only when two cannot hold a single round of keys.
-static PartPlan make_plan(uint32_t m, uint32_t k) {
+// fixed: the batch has a compile-time key length (pick_fmt > 0), which allows more stash rounds
+// for some k (build_rounds_max).
+static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     PartPlan pl{};
     pl.k = k;
     pl.m = m;
@@ -596,19 +605,20 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
     // runtime k (the K = 0 kernel) keeps kStash / k rounds; compiled K values their own
     const bool ck = k == 4 || k == 9 || k == 10 || k == 19;
-    const uint32_t rmax = (uint32_t)(ck ? build_rounds_max((int)k) : rounds_max((int)k));
+    const uint32_t rmax = (uint32_t)(ck ? build_rounds_max((int)k, fixed) : rounds_max((int)k));
+    const uint32_t kpr = kPBlock / (uint32_t)(ck ? build_spl((int)k, fixed) : 1);  // keys per round
     for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
         const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)pl.nseg_pad;
         // LDS = 2.5 * CP with CP <= C + nseg + 8
         const int64_t cmax = avail * 2 / 5 - pl.nseg - 8;
-        const int64_t kt = std::min<int64_t>((int64_t)rmax * kPBlock, cmax / k);
-        if (kt >= kPBlock || per_cu == 1) {
+        const int64_t kt = std::min<int64_t>((int64_t)rmax * kpr, cmax / k);
+        if (kt >= kpr || per_cu == 1) {
             pl.KT = (uint32_t)std::max<int64_t>(kt, 1);
             break;
         }
     }
-    pl.R = (pl.KT + kPBlock - 1) / kPBlock;
+    pl.R = (pl.KT + kpr - 1) / kpr;
     pl.C = pl.KT * k;
     pl.CP = (pl.C + pl.nseg + 7) & ~7u;
     pl.tile_words = pl.CP / 2 + pl.CP / 8;
@@ -641,8 +651,11 @@ static PartPlan make_plan(uint32_t m, uint32_t k) {
 
 bool partition_supported(uint32_t m, uint32_t k) {
     if (m == 0 || k < 1 || k > (uint32_t)kStash) return false;
-    const PartPlan pl = make_plan(m, k);
-    return pl.lds1 <= kLdsPerCu && pl.CP <= 65535;
+    for (bool fixed : {true, false}) {
+        const PartPlan pl = make_plan(m, k, fixed);
+        if (pl.lds1 > kLdsPerCu || pl.CP > 65535) return false;
+    }
+    return true;
 }
 
 static uint64_t chunk_keys_for(const PartPlan& pl, uint64_t n) {
@@ -653,16 +666,21 @@ static uint64_t chunk_keys_for(const PartPlan& pl, uint64_t n) {
 // Bytes of workspace one launch_build_partitioned call needs for n keys.
 uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     if (!partition_supported(m, k)) return 0;
-    const PartPlan pl = make_plan(m, k);
-    const uint64_t ntiles = (chunk_keys_for(pl, n) + pl.KT - 1) / pl.KT;
-    return ntiles * ((uint64_t)pl.tile_words * 4 + (uint64_t)pl.nseg * 4) + 512;
+    uint64_t need = 0;
+    for (bool fixed : {true, false}) {  // the larger of the two layouts' plans
+        const PartPlan pl = make_plan(m, k, fixed);
+        const uint64_t ntiles = (chunk_keys_for(pl, n) + pl.KT - 1) / pl.KT;
+        need = std::max<uint64_t>(need, ntiles * ((uint64_t)pl.tile_words * 4 + (uint64_t)pl.nseg * 4) + 512);
+    }
+    return need;
 }
 
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
                                     void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s) {
     if (kb.n == 0 || k == 0) return hipSuccess;
     if (!partition_supported(m, k)) return hipErrorInvalidValue;
-    PartPlan pl = make_plan(m, k);
+    // every chunk keeps the batch's alignment (chunks are whole tiles of keys), so one layout
+    PartPlan pl = make_plan(m, k, pick_fmt(kb.keys, kb.offsets, kb.stride) > 0);
     const uint64_t chunk_keys = chunk_keys_for(pl, kb.n);
     const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
     if (ws_bytes < partition_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;

@@ -31,10 +31,21 @@ constexpr uint32_t kShortRun = 24;  // mean entries per (tile, segment) run belo
 // Rounds of 1024 keys a lane can stash: kStash / k indices, but k = 4 keeps 24 so the fully
 // unrolled K = 4 kernel stays within 64 VGPRs (two workgroups per CU) without spilling.
 __host__ __device__ constexpr int rounds_max(int k) { return k == 4 ? 6 : kStash / k; }
-// Stash rounds of the build kernels.  (Two rounds for K = 19, velarixdb's default p = 1e-4,
-// would fill the tile's LDS image -- ~1 600 keys instead of 1 024 -- but 38 stashed indices
-// spill past the 64 VGPRs that two workgroups per CU allow; measured, not kept.)
-__host__ __device__ constexpr int build_rounds_max(int k) { return rounds_max(k); }
+// Lanes per key of the build kernels: K = 19 (velarixdb's default p = 1e-4) with a compile-time
+// key length splits a key's seeds over two lanes (0..9 and 10..18).  One lane per key stashes 19
+// indices per round and fits one round (1 024 keys) in the 64 VGPRs two workgroups per CU allow,
+// while the tile's LDS image holds ~1 500 keys: ~11-entry runs for k_seg_or.  Two lanes per key
+// stash 10 each, three rounds of 512 keys, and fill the image (the seed-independent prefix is
+// absorbed twice: +3 % hashing).  Runtime-length layouts keep more live state and would spill:
+// they stay at one lane per key.
+__host__ __device__ constexpr int build_spl(int k, bool fixed) { return (k == 19 && fixed) ? 2 : 1; }
+// Seeds per lane and stash rounds of the build kernels.
+__host__ __device__ constexpr int build_kl(int k, bool fixed) {
+    return (k + build_spl(k, fixed) - 1) / build_spl(k, fixed);
+}
+__host__ __device__ constexpr int build_rounds_max(int k, bool fixed) {
+    return build_spl(k, fixed) == 1 ? rounds_max(k) : kStash / build_kl(k, fixed);
+}
 
 // Exclusive scan of v[0..n) in LDS (n <= 4 * kPBlock).
 __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, uint32_t* wsum) {
