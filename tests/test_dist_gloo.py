@@ -70,3 +70,12 @@ def test_shard_range_covers_everything():
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
             assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
+
+
+def test_or_words_dev_rejects_mismatched_tensors():
+    """shape / dtype / contiguity mismatches are Python errors, never a kernel reading
+    past a buffer (checked before anything reaches the device)."""
+    from velarixdb_amd.dist import or_words_dev
+    a = torch.zeros(8, dtype=torch.int32)
+    with pytest.raises(ValueError, match="device tensors"):
+        or_words_dev(a, a)

@@ -276,3 +276,18 @@ def test_multi_probe_zero_bit_filter_with_ranges(vbf):
     assert got[:, 0].tolist()[:2] == [True, True] and not got[:, 1].any()
     with pytest.raises(ZeroDivisionError):
         candidates([b"a1", b"m5"], ranges)
+
+
+def test_or_words_dev_argument_checks(vbf):
+    """a shorter, strided or wrongly typed src is a ValueError, not a GPU fault."""
+    from velarixdb_amd.dist import or_words_dev
+    a = torch.zeros(64, dtype=torch.int32, device="cuda:0")
+    for bad in (torch.zeros(32, dtype=torch.int32, device="cuda:0"),
+                torch.zeros(128, dtype=torch.int32, device="cuda:0")[::2],
+                torch.zeros(64, dtype=torch.int64, device="cuda:0")):
+        with pytest.raises(ValueError):
+            or_words_dev(a, bad)
+    b = torch.arange(64, dtype=torch.int32, device="cuda:0")
+    or_words_dev(a, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

@@ -237,3 +237,22 @@ def test_uniform_guess_cannot_be_fooled(vbf, ora):
     tomb = np.zeros(n, np.uint8)
     data, index = ora.sst_write(keys, offs, val, created, tomb)
     _same(vbf.sst.load_entries(data, index), (keys, offs, val, created, tomb))
+
+
+def test_dense_block_is_a_distinct_error(vbf, ora):
+    """a block with more than 256 entries (only hand-written files: the reference's
+    4096-byte blocks hold at most 4096 / 17 = 240, block_manager.rs:121-125) is reported with
+    its own message, never decoded wrongly; the same entries in reference-sized blocks decode."""
+    from velarixdb_amd import VbfError
+    n = 300
+    entry = (0).to_bytes(4, "little") + (7).to_bytes(4, "little") + (1720785462000).to_bytes(8, "little") + b"\0"
+    data = entry * n  # 300 empty-key entries, 5100 bytes, in ONE block
+    index = (0).to_bytes(4, "little") + (0).to_bytes(4, "little")  # one index record -> block at 0
+    with pytest.raises(VbfError, match="more than 256 entries"):
+        vbf.sst.load_entries(data, index)
+    # the reference writer's blocking of the same entries decodes, bit-exact
+    keys = np.zeros(1, np.uint8)
+    offs = np.zeros(n + 1, np.uint64)
+    good, gidx = ora.sst_write(keys, offs, np.full(n, 7, np.uint32), np.full(n, 1720785462000, np.uint64),
+                               np.zeros(n, np.uint8))
+    _same(vbf.sst.load_entries(good, gidx), ora.sst_decode(good))

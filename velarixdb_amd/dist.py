@@ -28,6 +28,14 @@ def or_words_dev(acc, src):
     """acc |= src on the GPU (HIP kernel vbf_or_words_dev); same-shape int32 device tensors."""
     if acc.device.type != "cuda" or src.device.type != "cuda":
         raise ValueError("or_words_dev needs device tensors (the OR runs as a HIP kernel)")
+    if acc.device != src.device:
+        raise ValueError("or_words_dev: acc on %s, src on %s" % (acc.device, src.device))
+    if acc.dtype != torch.int32 or src.dtype != torch.int32:
+        raise ValueError("or_words_dev needs int32 words (got %s, %s)" % (acc.dtype, src.dtype))
+    if acc.shape != src.shape:
+        raise ValueError("or_words_dev: shapes differ (%s vs %s)" % (tuple(acc.shape), tuple(src.shape)))
+    if not (acc.is_contiguous() and src.is_contiguous()):
+        raise ValueError("or_words_dev needs contiguous tensors")
     stream = ctypes.c_void_p(torch.cuda.current_stream(acc.device).cuda_stream)
     call("vbf_or_words_dev", ctypes.c_void_p(acc.data_ptr()), ctypes.c_void_p(src.data_ptr()), acc.numel(), stream)
 
