@@ -117,10 +117,13 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32
 VALU_PER_KEY_CFG2 = 1611.0
 
 
-# rocprofv3 names of the default build's kernels and the summary of the same command
-ROCPROF_KERNELS = {"tile_sort": "k_tile_pack<16, true, 10, true>", "transpose": "k_transpose_u16",
-                   "seg_or": "k_seg_or<3, 1024, 5>"}
-ROCPROF_SUMMARY = "profiles/r01/bench_default_kernel_stats.csv"
+# rocprofv3 names of the build's kernels, and the summary of the same command, per (key bytes, k)
+ROCPROF = {
+    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true>", "transpose": "k_transpose_u16",
+                "seg_or": "k_seg_or<3, 1024, 5>"}, "profiles/r02/bench_default_kernel_stats.csv"),
+    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true>", "transpose": "k_transpose_u16",
+                "seg_or": "k_seg_or<6, 1024, 4>"}, "profiles/r02/bench_k19_kernel_stats.csv"),
+}
 
 
 def pmc_traffic(name):
@@ -398,8 +401,8 @@ def bench_fixed(ctx, args):
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": dom, "kernel_ms": dom_s * 1e3,
                      "build_ms": kavg * 1e3, "build_frac": n * bytes_per_key / kavg / 1e9 / HBM_PEAK_GBS,
-                     "rocprof_kernels": ROCPROF_KERNELS,
-                     "rocprof_summary": ROCPROF_SUMMARY,
+                     "rocprof_kernels": ROCPROF.get((L, k), (None, None))[0],
+                     "rocprof_summary": ROCPROF.get((L, k), (None, None))[1],
                      "valu_frac_est": (n * VALU_PER_KEY_CFG2 / dom_s / VALU_PEAK_LANE_OPS
                                        if (L, k) == (16, 10) else None),
                      "algorithmic_bytes_per_key": bytes_per_key,

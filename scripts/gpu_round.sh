@@ -44,7 +44,11 @@ for s in $STEPS; do
     sst)    run bench_sst 600 python bench.py --sst --steps 5 --warmup 1 ;;
     compact) run bench_compact 600 python bench.py --compact --steps 5 --warmup 1 ;;
     multi)  run bench_multi 600 python bench.py --multi --steps 5 --warmup 1 ;;
-    e2e)    run bench_e2e 600 python bench.py --e2e --steps 3 --warmup 1 ;;
+    e2e)    run bench_e2e 600 python bench.py --e2e --steps 5 --warmup 1 ;;
+    e2efresh) run bench_e2e_fresh 600 python bench.py --e2e --e2e-fresh-out --steps 5 --warmup 1 ;;
+    memtable) run bench_memtable 300 python bench.py --memtable ;;
+    prof19) (cd /tmp && run prof19 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 20 --warmup 3 --no-cpu-baseline) || exit $? ;;
+    profmulti) (cd /tmp && run profmulti 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmulti" -o run -- python3 "$ROOT/bench.py" --multi --steps 10 --warmup 2) || exit $? ;;
     dist2spawn) run bench_dist2_spawn 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;
     residency) run pytest_residency 600 python -u -m pytest tests/test_gpu_residency.py -x -v -m gpu --timeout 120 --timeout-method thread ;;
     dist2)  run bench_dist2 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;

@@ -13,7 +13,9 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstdio>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -251,29 +253,80 @@ int do_probe(const vbf::KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* wo
 constexpr uint64_t kChunkBytes = 64ull << 20;
 
 // Host copy into / out of the pinned staging buffers, split over up to 8 threads
-// (VBF_COPY_THREADS): one thread's memcpy into pinned memory runs well below the PCIe rate.
-void par_memcpy(void* dst, const void* src, size_t n) {
-    constexpr size_t kMinPerThread = 4u << 20;
-    static const unsigned nt_max = [] {
+// (VBF_COPY_THREADS): one thread's memcpy into pinned memory runs well below the PCIe rate.  The
+// helper threads are a persistent pool (creating 7 threads per 16 MiB chunk cost ~0.1 ms each
+// chunk); concurrent callers take turns.
+class CopyPool {
+  public:
+    static CopyPool& get() {
+        static CopyPool* p = new CopyPool();  // never destroyed: workers outlive static teardown
+        return *p;
+    }
+    unsigned threads() const { return nt_; }
+    // Runs f(0 .. parts-1) with part 0 on the calling thread.
+    template <class F>
+    void run(unsigned parts, F&& f) {
+        std::lock_guard<std::mutex> caller(call_mu_);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = [&f](unsigned i) { f(i); };
+            parts_ = parts;
+            next_ = 1;
+            done_ = 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return done_ == parts_; });
+        job_ = nullptr;
+    }
+
+  private:
+    CopyPool() {
         const char* e = getenv("VBF_COPY_THREADS");
         const unsigned hw = std::thread::hardware_concurrency();
         const int v = e ? atoi(e) : (int)std::min(8u, hw ? hw : 1u);
-        return (unsigned)std::max(1, v);
-    }();
-    const unsigned nt = (unsigned)std::min<size_t>(nt_max, n / kMinPerThread);
+        nt_ = (unsigned)std::max(1, v);
+        for (unsigned t = 1; t < nt_; ++t) std::thread([this] { loop(); }).detach();
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            while (next_ < parts_) {
+                const unsigned i = next_++;
+                auto job = job_;
+                lk.unlock();
+                job(i);
+                lk.lock();
+                if (++done_ == parts_) done_cv_.notify_one();
+            }
+        }
+    }
+    unsigned nt_ = 1;
+    std::mutex call_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    std::function<void(unsigned)> job_;
+    unsigned parts_ = 0, next_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+};
+
+void par_memcpy(void* dst, const void* src, size_t n) {
+    constexpr size_t kMinPerThread = 2u << 20;
+    CopyPool& pool = CopyPool::get();
+    const unsigned nt = (unsigned)std::min<size_t>(pool.threads(), n / kMinPerThread);
     if (nt <= 1) {
         std::memcpy(dst, src, n);
         return;
     }
     const size_t per = (n / nt + 4095) & ~(size_t)4095;
-    std::vector<std::thread> th;
-    th.reserve(nt);
-    for (unsigned t = 1; t < nt && t * per < n; ++t) {
-        const size_t a = t * per, len = std::min(per, n - a);
-        th.emplace_back([=] { std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, len); });
-    }
-    std::memcpy(dst, src, std::min(per, n));
-    for (auto& x : th) x.join();
+    pool.run(nt, [=](unsigned t) {
+        const size_t a = (size_t)t * per;
+        if (a < n) std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, std::min(per, n - a));
+    });
 }
 
 struct Staging {
@@ -323,6 +376,8 @@ struct Staging {
 // DMA of chunk c+1 overlaps the (threaded) host copy of chunk c; pageable hipMemcpy runs at a
 // fraction of the link rate.  Small copies go direct.  Caller holds st.mu and has ordered src.
 constexpr uint64_t kXferDirect = 8ull << 20;
+// bounce chunk: small enough that the last chunk's host copy (not overlapped) is short
+constexpr uint64_t kXferChunk = 16ull << 20;
 
 int xfer_bufs(Staging& st) {
     for (int b = 0; b < 2; ++b)
@@ -342,18 +397,18 @@ int xfer_d2h(Staging& st, void* dst, const void* src, uint64_t bytes) {
     }
     int rc = xfer_bufs(st);
     if (rc) return rc;
-    const uint64_t nc = (bytes + kChunkBytes - 1) / kChunkBytes;
+    const uint64_t nc = (bytes + kXferChunk - 1) / kXferChunk;
     for (uint64_t c = 0; c <= nc; ++c) {
         if (c < nc) {
             const int b = (int)(c & 1);
-            const uint64_t off = c * kChunkBytes, len = std::min<uint64_t>(kChunkBytes, bytes - off);
+            const uint64_t off = c * kXferChunk, len = std::min<uint64_t>(kXferChunk, bytes - off);
             HIP_TRY(hipMemcpyAsync(st.h_xfer[b], static_cast<const char*>(src) + off, len, hipMemcpyDeviceToHost,
                                    st.stream[b]));
             HIP_TRY(hipEventRecord(st.done[b], st.stream[b]));
         }
         if (c > 0) {
             const int pb = (int)((c - 1) & 1);
-            const uint64_t off = (c - 1) * kChunkBytes, len = std::min<uint64_t>(kChunkBytes, bytes - off);
+            const uint64_t off = (c - 1) * kXferChunk, len = std::min<uint64_t>(kXferChunk, bytes - off);
             HIP_TRY(hipEventSynchronize(st.done[pb]));
             par_memcpy(static_cast<char*>(dst) + off, st.h_xfer[pb], len);
         }
@@ -369,10 +424,10 @@ int xfer_h2d(Staging& st, void* dst, const void* src, uint64_t bytes) {
     }
     int rc = xfer_bufs(st);
     if (rc) return rc;
-    const uint64_t nc = (bytes + kChunkBytes - 1) / kChunkBytes;
+    const uint64_t nc = (bytes + kXferChunk - 1) / kXferChunk;
     for (uint64_t c = 0; c < nc; ++c) {
         const int b = (int)(c & 1);
-        const uint64_t off = c * kChunkBytes, len = std::min<uint64_t>(kChunkBytes, bytes - off);
+        const uint64_t off = c * kXferChunk, len = std::min<uint64_t>(kXferChunk, bytes - off);
         if (c >= 2) HIP_TRY(hipEventSynchronize(st.done[b]));  // buffer b's previous DMA finished
         par_memcpy(st.h_xfer[b], static_cast<const char*>(src) + off, len);
         HIP_TRY(hipMemcpyAsync(static_cast<char*>(dst) + off, st.h_xfer[b], len, hipMemcpyHostToDevice, st.stream[b]));

@@ -161,28 +161,42 @@ __global__ __launch_bounds__(kPBlock) void k_group_out(const uint32_t* tiles, co
     const uint32_t* tl = tiles + (uint64_t)blockIdx.x * pl.cap;
     const uint32_t* rs = reinterpret_cast<const uint32_t*>(res + (uint64_t)blockIdx.x * pl.cap);
     const uint32_t full = g.G >= 8 ? 0xFFu : ((1u << g.G) - 1u);
-    for (uint32_t w = tid; w * 4 < total; w += kPBlock) {  // 4 entries per lane; cap % 32 == 0
+    // 4 entries per lane: one dword of result bytes and one 16-byte load of their entries (most
+    // entries of a multi-member group have some member's bit clear, so the entries are read
+    // unconditionally); cap % 32 == 0 keeps both aligned
+    for (uint32_t w = tid; w * 4 < total; w += kPBlock) {
         const uint32_t r = rs[w];
+        const uint4 ev = *reinterpret_cast<const uint4*>(tl + w * 4);
+        const uint32_t ee[4] = {ev.x, ev.y, ev.z, ev.w};
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const uint32_t e = w * 4 + c;
             const uint32_t b = (r >> (8 * c)) & full;
-            if (e < total && b != full) {  // some member's bit is clear: drop those members
-                const uint32_t local = tl[e] >> kByteSegBits;
+            if (w * 4 + c < total && b != full) {  // some member's bit is clear: drop those members
+                const uint32_t local = ee[c] >> kByteSegBits;
                 atomicAnd(&msk[local >> 2], ~(((~b) & full) << ((local & 3) * 8)));
             }
         }
     }
     __syncthreads();
+    // members in consecutive columns from an 8-aligned one and 8-byte rows: one 8-byte store per key
+    bool packed = g.G == 8 && (out_stride & 7u) == 0 && (g.col[0] & 7u) == 0 && !bounds &&
+                  (reinterpret_cast<uintptr_t>(out) & 7u) == 0;
+    for (uint32_t q = 1; q < g.G && packed; ++q) packed = g.col[q] == g.col[0] + q;
     for (uint32_t l = tid; l < nk; l += kPBlock) {
         const uint64_t j = key0 + l;
         const uint32_t mk = (msk[l >> 2] >> ((l & 3) * 8)) & 0xFFu;
         uint8_t* row = out + j * out_stride;
-        if (bounds) {
+        if (packed) {
+            // byte q = bit q of mk: spread the 8 bits to the low bit of 8 bytes
+            uint64_t v = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v |= (uint64_t)((mk >> q) & 1u) << (8 * q);
+            *reinterpret_cast<uint64_t*>(row + g.col[0]) = v;
+        } else if (bounds) {
             const uint8_t* kp;
             uint64_t kl;
             if (dk.offsets) {
-                kp = dk.keys + (dk.offsets[l + key0] - dk.off_base);
+                kp = dk.keys + (dk.offsets[j] - dk.off_base);
                 kl = dk.offsets[j + 1] - dk.offsets[j];
             } else {
                 kp = dk.keys + j * dk.stride;
