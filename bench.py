@@ -32,8 +32,8 @@ def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1)")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
                     help="BASELINE config (default: 2 on one GPU, 4 on several)")
     ap.add_argument("--keys", type=int, default=None)
