@@ -32,7 +32,7 @@ def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1)")
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
                     help="BASELINE config (default: 2 on one GPU, 4 on several)")
@@ -167,7 +167,10 @@ class Ctx:
                              % (self.local_world, ndev))
         torch.cuda.set_device(self.local)
         self.dev = torch.device("cuda", self.local)
-        if self.world > 1:
+        # VBF_FORCE_PG=1: join a process group even alone, so a one-GPU box exercises the RCCL
+        # calls of the N > 1 path (init, all_gather_object, all_reduce, barrier) for real
+        self.pg = self.world > 1 or os.environ.get("VBF_FORCE_PG") == "1"
+        if self.pg:
             if self.backend == "nccl":
                 dist.init_process_group("nccl", device_id=self.dev)
             else:
@@ -187,7 +190,7 @@ class Ctx:
     def _topology(self):
         """Every rank's device; with one rank per GPU no two ranks may share a card."""
         mine = self._device_info()
-        if self.world == 1:
+        if not self.pg:
             return {"world_size": 1, "backend": None, "ranks": [mine]}
         allr = [None] * self.world
         dist.all_gather_object(allr, mine)
@@ -208,25 +211,25 @@ class Ctx:
         return topo
 
     def barrier(self):
-        if self.world > 1:
+        if self.pg:
             dist.barrier()
 
     def _reduce(self, x, op):
-        if self.world == 1:
+        if not self.pg:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=self.dev if self.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=op)
         return float(t.item())
 
     def max_over_ranks(self, x):
-        return self._reduce(x, dist.ReduceOp.MAX if self.world > 1 else None)
+        return self._reduce(x, dist.ReduceOp.MAX)
 
     def sum_over_ranks(self, x):
-        return self._reduce(x, dist.ReduceOp.SUM if self.world > 1 else None)
+        return self._reduce(x, dist.ReduceOp.SUM)
 
     def gather(self, obj):
         """Every rank's `obj`, in rank order (on every rank)."""
-        if self.world == 1:
+        if not self.pg:
             return [obj]
         out = [None] * self.world
         dist.all_gather_object(out, obj)
@@ -829,7 +832,7 @@ def main():
         res = bench_fixed(ctx, args)
     if ctx.rank == 0:
         print(json.dumps(res), flush=True)
-    if ctx.world > 1:
+    if ctx.pg:
         dist.destroy_process_group()
 
 

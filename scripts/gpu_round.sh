@@ -50,6 +50,7 @@ for s in $STEPS; do
     prof19) (cd /tmp && run prof19 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 20 --warmup 3 --no-cpu-baseline) || exit $? ;;
     profmulti) (cd /tmp && run profmulti 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmulti" -o run -- python3 "$ROOT/bench.py" --multi --steps 10 --warmup 2) || exit $? ;;
     dist2spawn) run bench_dist2_spawn 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    rccl1) run bench_rccl1 300 env VBF_FORCE_PG=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 50 --no-cpu-baseline ;;
     residency) run pytest_residency 600 python -u -m pytest tests/test_gpu_residency.py -x -v -m gpu --timeout 120 --timeout-method thread ;;
     dist2)  run bench_dist2 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;
     ubench) run ubench 300 ./tools/ubench ;;
