@@ -59,7 +59,23 @@ __host__ __device__ __forceinline__ void sip_compress(Sip& s, uint64_t m) {
     s.v0 ^= m;
 }
 
-// Final block b (length byte << 56 | tail bytes) + d = 3 finalization rounds.
+// a ^ b ^ c in one v_bitop3_b32 per 32-bit half on gfx950 (truth table 0x96)
+__host__ __device__ __forceinline__ uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
+__host__ __device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+    return ((uint64_t)xor3_32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+           xor3_32((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
+
+// Final block b (length byte << 56 | tail bytes) + d = 3 finalization rounds.  The last round is
+// written out to what reaches the output v0 ^ v1 ^ v2 ^ v3: with v0' = swap32(v0) + v3r and
+// v3' = rotl21(v3r) ^ v0', v0' cancels (v0' ^ v3' = rotl21(v3r)), so the result is
+// rotl21(v3r) ^ rotl17(v1r) ^ v2' ^ swap32(v2') -- one v_bitop3 and one v_xor per half.
 __host__ __device__ __forceinline__ uint64_t sip_finish(Sip s, uint64_t b) {
     s.v3 ^= b;
     sip_round(s);
@@ -67,8 +83,12 @@ __host__ __device__ __forceinline__ uint64_t sip_finish(Sip s, uint64_t b) {
     s.v2 ^= 0xff;
     sip_round(s);
     sip_round(s);
-    sip_round(s);
-    return s.v0 ^ s.v1 ^ s.v2 ^ s.v3;
+    s.v0 += s.v1;
+    const uint64_t v1r = rotl64<13>(s.v1) ^ s.v0;
+    s.v2 += s.v3;
+    const uint64_t v3r = rotl64<16>(s.v3) ^ s.v2;
+    const uint64_t v2n = s.v2 + v1r;
+    return xor3_64(rotl64<21>(v3r), rotl64<17>(v1r), v2n) ^ swap32(v2n);
 }
 
 // State after absorbing every full block of the seed-independent prefix

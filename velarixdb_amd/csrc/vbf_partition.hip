@@ -85,6 +85,14 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
     __syncthreads();
 }
 
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ void lds_add(lds_u32* p) {
+    (void)__hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_add_rtn(lds_u32* p) {
+    return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // K > 0: k known at compile time (the stash and seed loops unroll, no indexed register moves);
 // K == 0: any k <= kStash at run time.  __launch_bounds__(1024, 8): two workgroups per CU (the
 // hashing of one overlaps the other's sort), i.e. at most 64 VGPRs; the offsets-layout kernels
@@ -92,12 +100,19 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
 template <int FMT, bool LP, int K, bool M31>
 __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan pl, uint32_t* tiles,
                                                        uint16_t* ends) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // CP entries
-    uint32_t* hi = smem + pl.CP / 2;                    // CP/8 words, 8 nibbles each
-    uint32_t* cnt = hi + pl.CP / 8;                     // nseg_pad
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
+    // The per-segment counters first, at LDS address 0 (the kernel has no static LDS, so the
+    // dynamic allocation starts there; launch_build_partitioned checks it): the count and rank
+    // atomics address them through an LDS-space pointer to 0, so a counter's address is the
+    // segment number times 4 with no base to add -- one VALU instruction fewer per bit index in
+    // each of the two passes.  Then the tile image, 16-byte aligned.
+    uint32_t* cnt = smem_all;                           // nseg_pad
+    lds_u32* const cnt0 = reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(0));  // == cnt
     uint32_t* wsum = cnt + pl.nseg_pad;                 // 16
     uint32_t* lhist = wsum + 16;                        // kLenBuckets (offsets layout)
+    uint32_t* smem = lhist + kLenBuckets;               // the image: (nseg_pad + 48) * 4 % 16 == 0
+    uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // CP entries
+    uint32_t* hi = smem + pl.CP / 2;                    // CP/8 words, 8 nibbles each
     const uint32_t tid = threadIdx.x;
     // Stagger (speed only): the second workgroup dispatched to each CU starts ~half a tile
     // later, so the two co-resident workgroups alternate hashing (VALU) and sorting (LDS)
@@ -174,7 +189,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
                 uint32_t idx = kSentinel;
                 if (valid && (SPL == 1 || seed0 + i < (uint32_t)K)) {
                     idx = mod_m<M31>(prefix_hash(p, seed0 + i), pl.m, pl.mu);
-                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    lds_add(&cnt0[idx >> kSegBits]);
                 }
                 stash[r * KL + i] = idx;
             }
@@ -194,7 +209,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
-                    atomicAdd(&cnt[idx >> kSegBits], 1u);
+                    lds_add(&cnt0[idx >> kSegBits]);
                 }
                 stash[ns++] = idx;
             }
@@ -221,7 +236,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> kSegBits], 1u) : 0u;
+            pos[q] = val[q] != kSentinel ? lds_add_rtn(&cnt0[val[q] >> kSegBits]) : 0u;
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -708,8 +723,13 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                                : k_tile_pack<FMT, LP, 0, false>;
             };
             auto fn = m <= (1u << 31) ? pick.template operator()<true>() : pick.template operator()<false>();
-            err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
+            // the segment counters sit at LDS address 0: no static LDS may precede them
+            hipFuncAttributes fa{};
+            err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
+            if (err == hipSuccess && fa.sharedSizeBytes != 0) err = hipErrorInvalidKernelFile;
+            if (err == hipSuccess)
+                err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
             if (err == hipSuccess)
                 hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
         });
