@@ -1407,17 +1407,18 @@ int vbf_filter_migrate(vbf_filter* f, int device) {
     uint32_t* nd = nullptr;
     if (device != VBF_DEVICE_HOST && s.nwords) {
         DEVICE_SCOPE(device);
-        HIP_TRY(hipMalloc((void**)&nd, s.nwords * 4));
-        const hipError_t e = hipMemcpy(nd, w.data(), s.nwords * 4, hipMemcpyHostToDevice);
-        if (e != hipSuccess) {
-            (void)hipFree(nd);
+        hipError_t e = hipMalloc((void**)&nd, s.nwords * 4);
+        if (e == hipSuccess) e = hipMemcpy(nd, w.data(), s.nwords * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {  // the filter stays where it was, bits intact
+            if (nd) (void)hipFree(nd);
             if (s.host()) s.h_words.swap(w);
-            return fail(VBF_EHIP, "hipMemcpy to device %d: %s", device, hipGetErrorString(e));
+            return fail(e == hipErrorOutOfMemory ? VBF_ENOMEM : VBF_EHIP, "moving the bits to device %d: %s",
+                        device, hipGetErrorString(e));
         }
     }
     if (!s.host()) {  // release the old device copy (its work is finished: storage_sync above)
         DEVICE_SCOPE(s.device);
-        if (s.d_words) HIP_TRY(hipFree(s.d_words));
+        if (s.d_words) (void)hipFree(s.d_words);
         if (s.last) (void)hipEventDestroy(s.last);
         s.last = nullptr;
         s.pending = false;
