@@ -126,6 +126,21 @@ ROCPROF = {
 }
 
 
+def pmc_sq(name):
+    """VALU issue busy and wait fractions of k_tile_pack from one rocprofv3 SQ pass
+    (tools/pmc_sq.py); the newest round's."""
+    for rnd in ("r02",):
+        path = os.path.join(ROOT, "profiles", rnd, name)
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            return {"valu_issue_busy": d["valu_issue_busy"], "wave_wait_any_frac": d["wave_wait_any_frac"],
+                    "source": "profiles/%s/%s" % (rnd, name)}
+        except (OSError, ValueError, KeyError):
+            continue
+    return None
+
+
 def pmc_traffic(name):
     """Per-launch HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes (the newest
     round's measurement)."""
@@ -408,6 +423,7 @@ def bench_fixed(ctx, args):
                      "rocprof_summary": ROCPROF.get((L, k), (None, None))[1],
                      "valu_frac_est": (n * VALU_PER_KEY_CFG2 / dom_s / VALU_PEAK_LANE_OPS
                                        if (L, k) == (16, 10) else None),
+                     "sq_counters": pmc_sq("sq_tile_pack.json") if (n, L, k) == (100_000_000, 16, 10) else None,
                      "algorithmic_bytes_per_key": bytes_per_key,
                      "siprounds_per_key": (L + 8) // 8 + 5 * k,
                      "phases": ph},
