@@ -112,6 +112,42 @@ __host__ __device__ __forceinline__ uint64_t prefix_hash(const Prefix& p, uint64
     return sip_finish(s, ((uint64_t)p.total << 56) | hi);
 }
 
+// The same hash when the prefix ends on a block boundary (P % 8 == 0: every compile-time key
+// length, 8/16/24/32 bytes with or without the length block), with the seed-independent half of
+// the first per-seed SipRound done once per key.  The seed block is the seed itself, so that
+// round's v0 += v1 / rotl13 / swap and rotl16(v3) do not depend on it: rotl16(v3 ^ seed) =
+// rotl16(v3) ^ (seed << 16) for seed < 2^16, and the swapped sum is paired for the next 64-bit
+// add once per key instead of once per seed.  Bit-identical to prefix_hash (tests/test_gpu_parity).
+struct SeedCtx {
+    uint64_t v2, v3, as, b1, r16, r17b;
+    uint32_t total;
+};
+__host__ __device__ __forceinline__ SeedCtx seed_ctx(const Prefix& p) {
+    SeedCtx q;
+    const uint64_t a = p.st.v0 + p.st.v1;
+    q.b1 = rotl64<13>(p.st.v1) ^ a;
+    q.as = swap32(a);
+    q.v2 = p.st.v2;
+    q.v3 = p.st.v3;
+    q.r16 = rotl64<16>(p.st.v3);
+    q.r17b = rotl64<17>(q.b1);
+    q.total = p.total;
+    return q;
+}
+__host__ __device__ __forceinline__ uint64_t seed_hash(const SeedCtx& q, uint32_t seed) {
+    const uint64_t c = q.v2 + (q.v3 ^ seed);                             // v2 += v3 ^ m
+    const uint64_t d = ((uint64_t)((uint32_t)(q.r16 >> 32) ^ (uint32_t)(c >> 32)) << 32) |
+                       xor3_32((uint32_t)q.r16, (uint32_t)c, seed << 16);  // rotl16(v3 ^ m) ^ v2
+    const uint64_t e = q.as + d;                                         // v0 += v3
+    Sip s;
+    s.v3 = rotl64<21>(d) ^ e;
+    const uint64_t g = c + q.b1;                                         // v2 += v1
+    s.v1 = q.r17b ^ g;
+    s.v2 = swap32(g);
+    s.v0 = e ^ seed;                                                     // v0 ^= m
+    return sip_finish(s, (uint64_t)q.total << 56);
+}
+
 // Same, with P % 8 known at compile time (fixed-length keys).
 template <uint32_t R>
 __device__ __forceinline__ uint64_t prefix_hash_c(const Sip& st, uint64_t tail, uint32_t total,

@@ -184,11 +184,16 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
                     p = key_prefix<FMT, LP>(dk, key_of(slot));
                 }
             }
+            // compile-time key lengths end the prefix on a block boundary: the seed loop shares
+            // half of its first SipRound (seed_hash, sip13.hpp)
+            SeedCtx q{};
+            if constexpr (FMT > 0) q = seed_ctx(p);
 #pragma unroll
             for (int i = 0; i < KL; ++i) {
                 uint32_t idx = kSentinel;
                 if (valid && (SPL == 1 || seed0 + i < (uint32_t)K)) {
-                    idx = mod_m<M31>(prefix_hash(p, seed0 + i), pl.m, pl.mu);
+                    const uint64_t h = FMT > 0 ? seed_hash(q, seed0 + i) : prefix_hash(p, seed0 + i);
+                    idx = mod_m<M31>(h, pl.m, pl.mu);
                     lds_add(&cnt0[idx >> kSegBits]);
                 }
                 stash[r * KL + i] = idx;

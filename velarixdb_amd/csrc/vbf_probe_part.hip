@@ -46,11 +46,13 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
             const bool valid = (uint32_t)r < pl.R && j < key_end;
             Prefix p{};
             if (valid) p = key_prefix<FMT, LP>(dk, j);
+            SeedCtx q{};
+            if constexpr (FMT > 0) q = seed_ctx(p);  // block-aligned prefix: seed_hash (sip13.hpp)
 #pragma unroll
             for (int i = 0; i < K; ++i) {
                 uint32_t idx = kSentinel;
                 if (valid) {
-                    idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
+                    idx = mod_m<M31>(FMT > 0 ? seed_hash(q, i) : prefix_hash(p, i), pl.m, pl.mu);
                     atomicAdd(&cnt[idx >> SB], 1u);
                 }
                 stash[r * K + i] = idx;
