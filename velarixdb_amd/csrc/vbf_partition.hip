@@ -40,6 +40,8 @@ struct PartPlan {
     uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or); 0 = by run length
     uint32_t len_order;   // offsets layout: deal keys to lanes by length (VBF_LEN_ORDER, default 1)
     uint32_t stage_keys;  // the lo16 image holds perm + (begin, length) per key (VBF_STAGE_KEYS)
+    uint32_t nsegS;       // row stride of ends[tile][seg] (nseg rounded up to 8: 16-byte rows)
+    uint32_t ntS;         // row stride of endsT[seg][tile] (tiles rounded up to 8)
     uint64_t m, mu, nwords;
 };
 
@@ -221,9 +223,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
         }
     }
     __syncthreads();
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = (cnt[s] + 1) & ~1u;  // even runs
-    __syncthreads();
-    block_exclusive_scan(cnt, pl.nseg, wsum);
+    block_exclusive_scan<true>(cnt, pl.nseg, wsum);  // starts of even-length runs
     __syncthreads();
     if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
         uint32_t acc = 0;
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     uint32_t* out_hi = out + pl.CP / 2;
     const uint32_t hi_words = (total + 7) / 8;
     for (uint32_t w = tid; w < hi_words; w += kPBlock) out_hi[w] = hi[w];
-    uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nseg;
+    uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nsegS;
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)((cnt[s] + 1) & ~1u);
 }
 
@@ -298,6 +298,54 @@ __global__ __launch_bounds__(256) void k_transpose_u16(const uint16_t* in, uint1
 
 void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t s) {
     hipLaunchKernelGGL(k_transpose_u16, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, s, in, out, rows, cols);
+}
+
+// in[rows][in_stride] -> out[cols][out_stride] with both strides multiples of 8 and 16-byte aligned
+// buffers: a 64 x 64 tile moves as 16-byte vectors (512 per tile, two per thread each way) instead
+// of 2-byte elements -- one eighth of the memory instructions (the build's k = 19 ends array is
+// 250 MB).  The vectors may cover stride padding past rows / cols: in stays inside in_stride,
+// out inside out_stride, and the padding is never read.  LDS rows of 66 u16 (33 dwords) keep the
+// column reads of the write phase on different banks.
+__global__ __launch_bounds__(256) void k_transpose_u16_v(const uint16_t* in, uint16_t* out, uint32_t rows,
+                                                         uint32_t cols, uint32_t in_stride, uint32_t out_stride) {
+    __shared__ uint32_t t[64 * 33];
+    const uint32_t c0 = blockIdx.x * 64, r0 = blockIdx.y * 64, tid = threadIdx.x;
+#pragma unroll
+    for (uint32_t q = tid; q < 512; q += 256) {
+        const uint32_t r = q >> 3, cv = (q & 7) * 8;
+        if (r0 + r < rows && c0 + cv < cols) {
+            const uint4 v = *reinterpret_cast<const uint4*>(in + (uint64_t)(r0 + r) * in_stride + c0 + cv);
+            uint32_t* d = t + r * 33 + cv / 2;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+    }
+    __syncthreads();
+    const uint16_t* t16 = reinterpret_cast<const uint16_t*>(t);
+#pragma unroll
+    for (uint32_t q = tid; q < 512; q += 256) {
+        const uint32_t c = q >> 3, rv = (q & 7) * 8;
+        if (c0 + c < cols && r0 + rv < rows) {
+            uint32_t w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                w[i] = (uint32_t)t16[(rv + 2 * i) * 66 + c] | ((uint32_t)t16[(rv + 2 * i + 1) * 66 + c] << 16);
+            *reinterpret_cast<uint4*>(out + (uint64_t)(c0 + c) * out_stride + r0 + rv) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+
+void launch_transpose_u16_strided(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols,
+                                  uint32_t in_stride, uint32_t out_stride, hipStream_t s) {
+    const bool vec = in_stride % 8 == 0 && out_stride % 8 == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    if (vec)
+        hipLaunchKernelGGL(k_transpose_u16_v, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, s, in, out,
+                           rows, cols, in_stride, out_stride);
+    else if (in_stride == cols && out_stride == rows)
+        launch_transpose_u16(in, out, rows, cols, s);
 }
 
 // OR 8 packed indices (8 u16 low halves + their 8 nibbles) into the segment bitmap.
@@ -373,8 +421,8 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
 
     const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / pl.G);
     const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / pl.G);
-    const uint16_t* row_end = endsT + (uint64_t)seg * ntiles;
-    const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * ntiles : nullptr;
+    const uint16_t* row_end = endsT + (uint64_t)seg * pl.ntS;
+    const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * pl.ntS : nullptr;
     const uint32_t grp = lane >> 3, q8 = (lane & 7) * 8;
     // a wave serves 8 * NG tiles per batch (8-lane groups, NG runs each)
     const uint32_t step = (BS / 64) * 8 * NG;
@@ -642,6 +690,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     pl.C = pl.KT * k;
     pl.CP = (pl.C + pl.nseg + 7) & ~7u;
     pl.tile_words = pl.CP / 2 + pl.CP / 8;
+    pl.nsegS = (pl.nseg + 7) & ~7u;
     pl.lds1 = (pl.CP / 2 + pl.CP / 8 + pl.nseg_pad + 16 + kLenBuckets) * 4;
     // VBF_TILE_LDS_MIN (experiments, speed only): request at least this much LDS per k_tile_pack
     // workgroup, e.g. > 80 KiB to hold one workgroup per CU
@@ -690,7 +739,8 @@ uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     for (bool fixed : {true, false}) {  // the larger of the two layouts' plans
         const PartPlan pl = make_plan(m, k, fixed);
         const uint64_t ntiles = (chunk_keys_for(pl, n) + pl.KT - 1) / pl.KT;
-        need = std::max<uint64_t>(need, ntiles * ((uint64_t)pl.tile_words * 4 + (uint64_t)pl.nseg * 4) + 512);
+        // tiles, then ends[ntiles][nsegS] and endsT[nsegS][ntiles rounded up to 8] (16-byte aligned)
+        need = std::max<uint64_t>(need, ntiles * (uint64_t)pl.tile_words * 4 + (ntiles + 8) * (uint64_t)pl.nsegS * 4 + 512);
     }
     return need;
 }
@@ -705,8 +755,9 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
     const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
     if (ws_bytes < partition_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;
     uint32_t* tiles = reinterpret_cast<uint32_t*>(ws);
-    uint16_t* ends = reinterpret_cast<uint16_t*>(tiles + max_tiles * pl.tile_words);
-    uint16_t* endsT = ends + max_tiles * pl.nseg;
+    uint16_t* ends = reinterpret_cast<uint16_t*>(
+        (reinterpret_cast<uintptr_t>(tiles + max_tiles * pl.tile_words) + 15) & ~(uintptr_t)15);
+    uint16_t* endsT = ends + max_tiles * pl.nsegS;  // nsegS % 8 == 0: stays 16-byte aligned
 
     for (uint64_t lo = 0; lo < kb.n; lo += chunk_keys) {
         const uint64_t cn = std::min<uint64_t>(chunk_keys, kb.n - lo);
@@ -741,7 +792,8 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         if (err != hipSuccess) return err;
         phase_end(kPhaseTileSort, s);
         phase_begin(kPhaseTranspose, s);
-        launch_transpose_u16(ends, endsT, ntiles, pl.nseg, s);
+        pl.ntS = (ntiles + 7) & ~7u;
+        launch_transpose_u16_strided(ends, endsT, ntiles, pl.nseg, pl.nsegS, pl.ntS, s);
         // several workgroups per segment when there are few segments (small m)
         pl.G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
         const bool merge = atomic_merge || pl.G > 1;

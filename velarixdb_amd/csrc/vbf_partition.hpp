@@ -47,7 +47,11 @@ __host__ __device__ constexpr int build_rounds_max(int k, bool fixed) {
     return build_spl(k, fixed) == 1 ? rounds_max(k) : kStash / build_kl(k, fixed);
 }
 
-// Exclusive scan of v[0..n) in LDS (n <= 4 * kPBlock).
+// Exclusive scan of v[0..n) in LDS (n <= 4 * kPBlock).  EVEN: scan the counts rounded up to even
+// (the build's even-length runs) in the same pass.  One barrier: after it every wave adds up the
+// totals of the waves before it itself instead of waiting for one wave to scan them.  The caller
+// synchronises before reading v[] or reusing wsum[].
+template <bool EVEN = false>
 __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, uint32_t* wsum) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t loc[4];
@@ -55,7 +59,8 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t s = tid * 4 + q;
-        loc[q] = s < n ? v[s] : 0;
+        const uint32_t c = s < n ? v[s] : 0;
+        loc[q] = EVEN ? (c + 1) & ~1u : c;
         sum += loc[q];
     }
     uint32_t incl = sum;
@@ -66,18 +71,12 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
     }
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    if (wave == 0) {
-        const uint32_t w = lane < kPBlock / 64 ? wsum[lane] : 0;
-        uint32_t wi = w;
+    static_assert(kPBlock / 64 <= 16, "one 16-lane group sums the wave totals");
+    uint32_t before = lane < wave ? wsum[lane] : 0u;  // lanes 0..15 hold the earlier waves' totals
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const uint32_t y = __shfl_up(wi, o);
-            if (lane >= (uint32_t)o) wi += y;
-        }
-        if (lane < kPBlock / 64) wsum[lane] = wi - w;
-    }
-    __syncthreads();
-    uint32_t run = wsum[wave] + incl - sum;
+    for (int o = 8; o; o >>= 1) before += __shfl_xor(before, o);
+    before = (uint32_t)__shfl((int)before, 0);
+    uint32_t run = before + incl - sum;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t s = tid * 4 + q;
@@ -88,6 +87,10 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
 
 // K2 (vbf_partition.hip): ends[rows][cols] -> endsT[cols][rows], shared by build and probe.
 void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t s);
+// The same with row strides (in: in_stride, out: out_stride elements); both multiples of 8 and
+// 16-byte aligned buffers take a 16-byte-vector kernel.
+void launch_transpose_u16_strided(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols,
+                                  uint32_t in_stride, uint32_t out_stride, hipStream_t s);
 
 // Partitioned probe plan (vbf_probe_part.hip): KT keys per tile, C = KT * k entries, segments of
 // 2^sb filter positions, `cap` padded entries per tile in the workspace.
