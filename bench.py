@@ -119,9 +119,9 @@ VALU_PER_KEY_CFG2 = 1611.0
 
 # rocprofv3 names of the build's kernels, and the summary of the same command, per (key bytes, k)
 ROCPROF = {
-    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true>", "transpose": "k_transpose_u16",
+    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true>", "transpose": "k_transpose_u16_v",
                 "seg_or": "k_seg_or<3, 1024, 5>"}, "profiles/r02/bench_default_kernel_stats.csv"),
-    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true>", "transpose": "k_transpose_u16",
+    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true>", "transpose": "k_transpose_u16_v",
                 "seg_or": "k_seg_or<6, 1024, 4>"}, "profiles/r02/bench_k19_kernel_stats.csv"),
 }
 
