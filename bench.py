@@ -48,6 +48,8 @@ def make_parser():
     ap.add_argument("--memtable", action="store_true",
                     help="single-key set/contains latency on a memtable-size filter (mem.rs:207-230)")
     ap.add_argument("--strategy", type=int, default=0, help="0 auto, 1 atomic, 2 partitioned")
+    ap.add_argument("--separate-zero", action="store_true",
+                    help="zero the filter with a fill kernel before each build instead of VBF_BUILD_FRESH")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000)
     ap.add_argument("--cpu-opt-threads", type=int, default=None,
@@ -251,6 +253,13 @@ class Ctx:
         return out
 
 
+def build_strategy(args):
+    """The build strategy flags of one timed step: a fresh filter (new + build) unless
+    --separate-zero asks for the zero fill as its own kernel."""
+    from velarixdb_amd._lib import VBF_BUILD_FRESH
+    return args.strategy if args.separate_zero else args.strategy | VBF_BUILD_FRESH
+
+
 def timed_steps(ctx, step, steps, warmup):
     """W untimed steps, then K steps bracketed by barrier + synchronize.
 
@@ -365,11 +374,14 @@ def bench_fixed(ctx, args):
     words = torch.empty(nwords, dtype=torch.int32, device=ctx.dev)
 
     def step(evs):
-        words.zero_()  # BloomFilter::new: BitVec::from_elem(m, false) (bf.rs:71)
+        # BloomFilter::new (BitVec::from_elem(m, false), bf.rs:71) + build_filter_from_entries:
+        # VBF_BUILD_FRESH writes every word of the filter (zeros included) in the build itself
+        if args.separate_zero:
+            words.zero_()
         if evs is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(ctx.stream)
-        call("vbf_build_dev_ex", vp(keys), None, L, n, 1, m, k, vp(words), args.strategy, ctx.sp)
+        call("vbf_build_dev_ex", vp(keys), None, L, n, 1, m, k, vp(words), build_strategy(args), ctx.sp)
         if evs is not None:
             b.record(ctx.stream)
             evs.append((a, b))
@@ -468,11 +480,12 @@ def bench_var(ctx, args):
     words = torch.empty((m + 31) // 32, dtype=torch.int32, device=ctx.dev)
 
     def step(evs):
-        words.zero_()
+        if args.separate_zero:
+            words.zero_()
         if evs is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(ctx.stream)
-        call("vbf_build_dev_ex", vp(keys), vp(off), 0, n, 1, m, k, vp(words), args.strategy, ctx.sp)
+        call("vbf_build_dev_ex", vp(keys), vp(off), 0, n, 1, m, k, vp(words), build_strategy(args), ctx.sp)
         if evs is not None:
             b.record(ctx.stream)
             evs.append((a, b))

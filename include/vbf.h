@@ -97,6 +97,12 @@ int vbf_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
 #define VBF_BUILD_AUTO 0
 #define VBF_BUILD_ATOMIC 1
 #define VBF_BUILD_PARTITIONED 2
+/* OR into a build strategy: `words` holds no filter yet -- BloomFilter::new (bf.rs:62-81, an
+ * all-zero BitVec) fused with build_filter_from_entries (bf.rs:126-128), as flush and compaction
+ * call them.  Every one of the ceil(m/32) words is written (prior contents ignored, the bits of
+ * keys set, all others 0), with no separate zero fill: the partitioned build's segment pass
+ * writes its segments without reading them first.  Without the flag a build ORs into `words`. */
+#define VBF_BUILD_FRESH 0x100
 int vbf_build_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                      int len_prefix, uint32_t m, uint32_t k, uint32_t* words, int strategy,
                      void* stream);

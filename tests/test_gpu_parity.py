@@ -488,3 +488,31 @@ def test_or_words_kernel(vbf):
         vbf._lib.call("vbf_or_words_dev", _ptr(a[1:]), _ptr(a[:8]), 8, _stream())
     with pytest.raises(ValueError):
         or_words_dev(torch.zeros(4, dtype=torch.int32), torch.zeros(4, dtype=torch.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,k,strategy", [
+    (200_000, 600_000_000, 10, PARTITIONED),  # one workgroup per segment: the fused path
+    (200_000, 600_000_000, 19, PARTITIONED),
+    (200_000, 10_000_000, 10, PARTITIONED),   # few segments, several workgroups each: zeroed first
+    (50_000, 600_000_000, 10, ATOMIC),        # zeroed first
+    (0, 1_000_003, 7, 0),                     # no keys: the new filter is all zeros
+])
+def test_fresh_build_ignores_prior_words(vbf, ora, n, m, k, strategy):
+    """VBF_BUILD_FRESH (BloomFilter::new + build_filter_from_entries, bf.rs:62-81,126-128): into
+    words full of garbage, the result is exactly the oracle's filter of the keys alone."""
+    from velarixdb_amd._lib import VBF_BUILD_FRESH
+    from velarixdb_amd.keys import HostBatch
+    L = 16
+    data = ora.gen_fixed(0x5EED0001, 0, max(n, 1), L)[: n * L]
+    b = HostBatch(data, None, L, n, 1)
+    nw = (m + 31) // 32
+    garbage = np.random.default_rng(7).integers(0, 2**32, nw, dtype=np.uint64).astype(np.uint32)
+    got = gpu_build(vbf, b, m, k, words=garbage, strategy=strategy | VBF_BUILD_FRESH)
+    if n == 0:
+        assert not got.any()
+        return
+    hs = (ora.hashes(b, k) % np.uint64(m)).ravel()
+    want = np.zeros(nw, np.uint32)
+    np.bitwise_or.at(want, (hs >> np.uint64(5)).astype(np.int64), (np.uint32(1) << (hs & np.uint64(31)).astype(np.uint32)))
+    assert np.array_equal(got, want)

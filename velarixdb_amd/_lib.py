@@ -21,6 +21,7 @@ VBF_DEVICE_HOST = -1
 VBF_BUILD_AUTO = 0
 VBF_BUILD_ATOMIC = 1
 VBF_BUILD_PARTITIONED = 2
+VBF_BUILD_FRESH = 0x100  # OR into a build strategy: BloomFilter::new fused with the build (vbf.h)
 
 _u8p = ctypes.c_void_p  # raw pointers (host or device) travel as integers
 _u64 = ctypes.c_uint64

@@ -162,7 +162,15 @@ constexpr uint64_t kMultiGroupMinKeys = 1ull << 20;
 // merges its segments with word atomics instead of load+store).
 int do_build(const vbf::KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, int strategy,
              bool atomic_merge, hipStream_t s) {
-    if (kb.n == 0 || k == 0) return VBF_OK;
+    const bool fresh = (strategy & VBF_BUILD_FRESH) != 0;
+    strategy &= ~VBF_BUILD_FRESH;
+    // a fresh filter the segment pass cannot write whole (atomic strategy, no keys, several
+    // chunks or several workgroups per segment) is zeroed first: BitVec::from_elem(m, false)
+    auto zero = [&]() -> int {
+        if (fresh && m) HIP_TRY(hipMemsetAsync(words, 0, ((uint64_t)m + 31) / 32 * 4, s));
+        return VBF_OK;
+    };
+    if (kb.n == 0 || k == 0) return zero();
     bool part;
     if (strategy == VBF_BUILD_ATOMIC) {
         part = false;
@@ -176,14 +184,18 @@ int do_build(const vbf::KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, i
         return fail(VBF_EINVAL, "unknown build strategy %d", strategy);
     }
     if (!part) {
+        if (int rc = zero()) return rc;
         HIP_TRY(vbf::launch_build(kb, m, k, words, s));
         return VBF_OK;
     }
+    const bool fused = fresh && !atomic_merge && vbf::partition_fresh_ok(kb.n, m, k);
+    if (fresh && !fused)
+        if (int rc = zero()) return rc;
     const uint64_t need = vbf::partition_workspace_bytes(kb.n, m, k);
     void* ws = nullptr;
     int rc = get_workspace(s, need, &ws);
     if (rc) return rc;
-    HIP_TRY(vbf::launch_build_partitioned(kb, m, k, words, ws, need, atomic_merge, s));
+    HIP_TRY(vbf::launch_build_partitioned(kb, m, k, words, ws, need, atomic_merge, s, fused));
     return VBF_OK;
 }
 

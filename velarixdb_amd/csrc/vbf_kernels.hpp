@@ -48,8 +48,13 @@ uint64_t probe_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
 hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
                                     unsigned long long* count, void* ws, uint64_t ws_bytes, hipStream_t s);
 uint64_t probe_count_partials(uint64_t n, uint32_t m, uint32_t k);
+// fresh: `words` holds no filter yet; the first chunk's segment pass writes every word without
+// reading it (callers zero the words themselves where that pass cannot own every segment).
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
-                                    void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s);
+                                    void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s,
+                                    bool fresh = false);
+// Whether a fresh build of n keys can skip the zero fill (one chunk, one workgroup per segment).
+bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k);
 hipError_t launch_probe(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
                         uint8_t* out, hipStream_t s);
 // Count: `partial` holds count_partials(n) u32 of scratch; the hits are added to *count.

@@ -40,6 +40,7 @@ struct PartPlan {
     uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or); 0 = by run length
     uint32_t len_order;   // offsets layout: deal keys to lanes by length (VBF_LEN_ORDER, default 1)
     uint32_t stage_keys;  // the lo16 image holds perm + (begin, length) per key (VBF_STAGE_KEYS)
+    uint32_t fresh;       // K3: the words hold no filter yet -- write the segment without reading it
     uint32_t nsegS;       // row stride of ends[tile][seg] (nseg rounded up to 8: 16-byte rows)
     uint32_t ntS;         // row stride of endsT[seg][tile] (tiles rounded up to 8)
     uint64_t m, mu, nwords;
@@ -406,7 +407,7 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
     const bool own = (pl.G == 1) && !atomic_merge;  // sole writer: start from the existing words
     for (uint32_t w = tid * 4; w < kSegWords; w += BS * 4) {
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (own && pl.ablate < 6) {
+        if (own && !pl.fresh && pl.ablate < 6) {
             if (w + 4 <= wn)
                 v = *reinterpret_cast<const uint4*>(words + wbase + w);
             else if (w < wn) {
@@ -745,8 +746,20 @@ uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     return need;
 }
 
+bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k) {
+    if (!partition_supported(m, k) || n == 0) return false;
+    for (bool fixed : {true, false}) {
+        const PartPlan pl = make_plan(m, k, fixed);
+        const uint64_t ck = chunk_keys_for(pl, n);
+        const uint64_t ntiles = (ck + pl.KT - 1) / pl.KT;
+        const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)ntiles, (512 + pl.nseg - 1) / pl.nseg));
+        if (ck < n || G > 1) return false;
+    }
+    return true;
+}
+
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
-                                    void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s) {
+                                    void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s, bool fresh) {
     if (kb.n == 0 || k == 0) return hipSuccess;
     if (!partition_supported(m, k)) return hipErrorInvalidValue;
     // every chunk keeps the batch's alignment (chunks are whole tiles of keys), so one layout
@@ -797,6 +810,9 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         // several workgroups per segment when there are few segments (small m)
         pl.G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
         const bool merge = atomic_merge || pl.G > 1;
+        // only the first chunk, and only where each segment has one sole writer, skips the read
+        pl.fresh = (fresh && lo == 0 && !merge) ? 1u : 0u;
+        if (fresh && lo == 0 && merge) return hipErrorInvalidValue;  // the caller zeroes first
         phase_end(kPhaseTranspose, s);
         phase_begin(kPhaseSegOr, s);
         // short runs (large k or m): the flattened variant; VBF_K3 overrides
