@@ -11,7 +11,7 @@ import csv
 import json
 import sys
 
-BUILD_KERNELS = ("k_tile_pack", "k_transpose_u16", "k_seg_or", "k_keys<(vbf::Op)0")
+BUILD_KERNELS = ("k_tile_pack", "k_transpose_u16_v", "k_seg_or", "k_keys<(vbf::Op)0")  # k_transpose_u16 (no _v): the probe's
 
 
 def per_kernel(path, counter):
