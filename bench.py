@@ -143,18 +143,22 @@ def pmc_sq(name):
     return None
 
 
-def pmc_traffic(name):
-    """Per-launch HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes (the newest
-    round's measurement)."""
+def pmc_traffic(name, kernel=None):
+    """HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes (the newest round's
+    measurement): (one launch of `kernel` -- read + write --, one whole build, source file)."""
     for rnd in ("r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             with open(path) as f:
                 d = json.load(f)
-            return d["per_launch_bytes"], "profiles/%s/%s" % (rnd, name)
+            per_kernel = None
+            for kname, kv in d.get("kernels", {}).items():
+                if kernel and kernel in kname:
+                    per_kernel = kv["read_bytes"] + kv["write_bytes"]
+            return per_kernel, d["per_launch_bytes"], "profiles/%s/%s" % (rnd, name)
         except (OSError, ValueError, KeyError):
             continue
-    return None, None
+    return None, None, None
 
 
 def vp(t):
@@ -408,8 +412,12 @@ def bench_fixed(ctx, args):
     dom = max(ph, key=lambda q: ph[q]["ms_per_launch"] * ph[q]["launches"]) if ph else None
     dom_s = ph[dom]["ms_per_launch"] / 1e3 if dom else kavg
     achieved = n * bytes_per_key / dom_s / 1e9
-    traffic, traffic_src = (pmc_traffic("traffic_config2.json") if (n, L, k) == (100_000_000, 16, 10)
-                            and args.strategy != 1 else (None, None))
+    # the contract's traffic: HBM bytes of one launch of the dominant kernel (like `achieved`);
+    # the whole build's bytes beside it
+    dom_kernel = (ROCPROF.get((L, k), ({}, None))[0] or {}).get(dom)
+    traffic, traffic_build, traffic_src = (pmc_traffic("traffic_config2.json", dom_kernel)
+                                           if (n, L, k) == (100_000_000, 16, 10) and args.strategy != 1
+                                           else (None, None, None))
     per_rank = ctx.gather({"rank": ctx.rank, "device": ctx.local, "keys": n, "seed": seed,
                            "keys_per_s": n * args.steps / rank_wall, "ms_per_step": rank_wall / args.steps * 1e3,
                            "fill_ratio": int(pop.item()) / m})
@@ -428,8 +436,8 @@ def bench_fixed(ctx, args):
                    "n_keys_per_gpu": n, "key_bytes": L, "m_bits": m, "k": k, "len_prefix": True,
                    "parallelism": "independent shards x%d" % ctx.world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": dom, "kernel_ms": dom_s * 1e3,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_build": traffic_build,
+                     "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_s * 1e3,
                      "build_ms": kavg * 1e3, "build_frac": n * bytes_per_key / kavg / 1e9 / HBM_PEAK_GBS,
                      "rocprof_kernels": ROCPROF.get((L, k), (None, None))[0],
                      "rocprof_summary": ROCPROF.get((L, k), (None, None))[1],
