@@ -14,6 +14,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
+FRESH = 0x100  # VBF_BUILD_FRESH
 
 
 def vp(t):
@@ -67,12 +68,60 @@ def test_config2_full_size_bit_exact(vbf, ora):
     assert count(vbf, keys, None, L, n, m, k, w_part) == n
     fill = popcount(vbf, w_part) / m
     assert abs(fill - (1 - math.exp(-k * n / m))) < 1e-3
+    # the benchmarked step (bench.py): BloomFilter::new fused with the build (VBF_BUILD_FRESH)
+    # into words holding garbage, the segment pass writing every word without reading it
+    w_fresh = torch.randint(-2**31, 2**31 - 1, (m // 32,), dtype=torch.int32, device=DEV)
+    build(vbf, keys, None, L, n, m, k, 2 | FRESH, words=w_fresh)
     # bit-exact against the oracle over the full 100M keys (16 host threads)
+    host = keys.cpu().numpy()
+    del keys, w_atom, w_again, w_split
+    want = ora.build_words(HostBatch(host, None, L, n, 1), m, k, threads=16)
+    assert np.array_equal(w_part.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(w_fresh.cpu().numpy().view(np.uint32), want)
+
+
+def test_config4_shard0_fresh_bit_exact(vbf, ora):
+    """Config 4's per-rank workload as bench.py --gpus N runs it on rank 0: SSTable shard 0,
+    50M x 16 B keys (seed 0x5EED0040), m = 5e8, k = 10, one fresh build (new + build fused,
+    the timed step) into garbage-filled words, bit-exact against the 16-thread oracle."""
+    from velarixdb_amd.keys import HostBatch
+    from velarixdb_amd.workloads import SEED_CFG4, fpr_for_bits_per_key
+    n, L = 50_000_000, 16
+    m = vbf.num_bits(n, fpr_for_bits_per_key(10))
+    k = vbf.num_hash_functions(m, n)
+    assert (m, k) == (500_000_000, 10)
+    keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG4 + 0, 0, n, L, vp(keys), sp())
+    words = torch.randint(-2**31, 2**31 - 1, ((m + 31) // 32,), dtype=torch.int32, device=DEV)
+    build(vbf, keys, None, L, n, m, k, 2 | FRESH, words=words)
+    assert count(vbf, keys, None, L, n, m, k, words) == n
     host = keys.cpu().numpy()
     del keys
     want = ora.build_words(HostBatch(host, None, L, n, 1), m, k, threads=16)
-    got = w_part.cpu().numpy().view(np.uint32)
-    assert np.array_equal(got, want)
+    assert np.array_equal(words.cpu().numpy().view(np.uint32), want)
+
+
+def test_config5_rank_shape_fresh(vbf):
+    """Config 5's per-rank shape on 8 GPUs: 125M x 32 B keys (1/8 of 1B), the saturated
+    m = 2^32 - 1 and k = 4 of the whole filter, a fresh partitioned build into garbage equal to
+    the per-key atomic build into zeros (the oracle would take minutes at this size; config 5's
+    sizing slice and the 5M-key oracle checks pin the 32-byte hash)."""
+    from velarixdb_amd.workloads import SEED_CFG5, fpr_for_bits_per_key
+    N = 1_000_000_000
+    m = vbf.num_bits(N, fpr_for_bits_per_key(15))
+    k = vbf.num_hash_functions(m, N)
+    assert (m, k) == (4294967295, 4)
+    n, L = 125_000_000, 32
+    keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG5, 0, n, L, vp(keys), sp())
+    nw = (m + 31) // 32
+    w_fresh = torch.randint(-2**31, 2**31 - 1, (nw,), dtype=torch.int32, device=DEV)
+    build(vbf, keys, None, L, n, m, k, 2 | FRESH, words=w_fresh)
+    w_atom = build(vbf, keys, None, L, n, m, k, 1)
+    assert torch.equal(w_fresh, w_atom)
+    assert count(vbf, keys, None, L, n, m, k, w_fresh) == n
+    fill = popcount(vbf, w_fresh) / m
+    assert abs(fill - (1 - math.exp(-k * n / m))) < 1e-3
 
 
 @pytest.mark.timeout(600)
@@ -91,11 +140,17 @@ def test_k19_full_size_bit_exact(vbf, ora):
     w_part = build(vbf, keys, None, L, n, m, k, 2)
     w_atom = build(vbf, keys, None, L, n, m, k, 1)
     assert torch.equal(w_part, w_atom)
+    del w_atom
+    # the benchmarked form (bench.py --bits-per-key 19): fresh build into garbage
+    w_fresh = torch.randint(-2**31, 2**31 - 1, ((m + 31) // 32,), dtype=torch.int32, device=DEV)
+    build(vbf, keys, None, L, n, m, k, 2 | FRESH, words=w_fresh)
+    assert torch.equal(w_fresh, w_part)
+    del w_fresh
     assert count(vbf, keys, None, L, n, m, k, w_part) == n
     fill = popcount(vbf, w_part) / m
     assert abs(fill - (1 - math.exp(-k * n / m))) < 1e-3
     host = keys.cpu().numpy()
-    del keys, w_atom
+    del keys
     want = ora.build_words(HostBatch(host, None, L, n, 1), m, k, threads=16)
     assert np.array_equal(w_part.cpu().numpy().view(np.uint32), want)
 
