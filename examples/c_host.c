@@ -9,7 +9,12 @@
  *   KEYS_FILE : N keys of STRIDE bytes, back to back (hashed as Vec<u8>: len_prefix = 1)
  *   writes OUT_PREFIX.words (the filter's u32 words), OUT_PREFIX.meta (16-byte filter.db),
  *   OUT_PREFIX.shards (words of two shard builds: first half / second half of the keys, at the
- *   same m and k) and prints one line: "m k hits n".
+ *   same m and k), OUT_PREFIX.filterdb (filter.db with the bit array persisted after the 16 bytes,
+ *   vbf_filter_serialize_ext) and prints one line: "m k hits n restored async_equal".
+ * The persisted file is read back (vbf_filter_recover_ext: restored = 1, same words, no rebuild),
+ * and a second filter is built with vbf_filter_set_host_async from the caller's buffer (released
+ * through the callback, as a Rust caller drops its packed Vec): async_equal = 1 when its words
+ * equal the synchronous build's.
  * Exit status 0 on success; any library failure prints vbf_last_error() and exits 1. */
 #include <stdint.h>
 #include <stdio.h>
@@ -24,6 +29,9 @@ static void check(int rc, const char* what) {
         exit(1);
     }
 }
+
+static int released = 0;
+static void release_keys(void* ctx) { released += (ctx != NULL); }
 
 static void write_file(const char* prefix, const char* ext, const void* p, size_t n) {
     char path[4096];
@@ -86,7 +94,33 @@ int main(int argc, char** argv) {
     check(vbf_build_shards_host(sh, 2, devs, 1), "vbf_build_shards_host");
     write_file(argv[5], "shards", sw, 2 * nw * 4);
 
-    printf("%u %u %llu %llu\n", m, k, (unsigned long long)hits, (unsigned long long)n);
+    /* filter.db with persisted bits (bf.rs:114-123 write + the extension), read back the way
+     * the lazy recovery of range.rs:117-128 would, without the rebuild */
+    uint64_t flen = 0;
+    check(vbf_filter_serialize_ext(f, NULL, NULL, 0, n, 1, NULL, 0, &flen), "serialize_ext(size)");
+    uint8_t* fdb = malloc(flen);
+    check(vbf_filter_serialize_ext(f, NULL, NULL, 0, n, 1, fdb, flen, &flen), "serialize_ext");
+    write_file(argv[5], "filterdb", fdb, flen);
+    vbf_filter* r = NULL;
+    int restored = 0;
+    check(vbf_filter_recover_ext(fdb, flen, 0, &r, &restored), "recover_ext");
+    uint32_t* rw = calloc(nw + 1, 4);
+    check(vbf_filter_words_to_host(r, rw, nw), "words(recovered)");
+    if (memcmp(rw, words, nw * 4) != 0 || vbf_filter_num_elements(r) != 2 * (uint32_t)n) restored = 0;
+
+    /* the asynchronous build from the caller's buffer */
+    vbf_filter* a = NULL;
+    check(vbf_filter_new(p, n, VBF_DEVICE_AUTO, &a), "vbf_filter_new(auto)");
+    check(vbf_filter_set_host_async(a, keys, NULL, stride, n, 1, release_keys, keys), "set_host_async");
+    check(vbf_filter_sync(a), "vbf_filter_sync");
+    check(vbf_filter_words_to_host(a, rw, nw), "words(async)");
+    const int async_equal = released == 1 && memcmp(rw, words, nw * 4) == 0;
+
+    printf("%u %u %llu %llu %d %d\n", m, k, (unsigned long long)hits, (unsigned long long)n, restored, async_equal);
+    vbf_filter_free(r);
+    vbf_filter_free(a);
+    free(fdb);
+    free(rw);
     vbf_filter_free(f);
     free(keys);
     free(hit);

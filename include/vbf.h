@@ -11,8 +11,11 @@
  *   BloomFilter::set                   src/filter/bf.rs:84-92      -> vbf_filter_set_host / _dev
  *   BloomFilter::contains              src/filter/bf.rs:95-105     -> vbf_filter_contains_host / _dev
  *   BloomFilter::build_filter_from_entries src/filter/bf.rs:126-128 -> vbf_filter_set_host (batch)
+ *                                                                     / vbf_filter_set_host_async
  *   BloomFilter::recover_meta          src/filter/bf.rs:135-150    -> vbf_filter_recover
  *   BloomFilter::serialize             src/filter/bf.rs:158-172    -> vbf_filter_serialize
+ *   BloomFilter::write + recover_meta + lazy rebuild, bits persisted (bf.rs:114-150,
+ *     range.rs:117-128)                                            -> vbf_filter_serialize_ext / _recover_ext
  *   FilterFileNode::recover            src/fs/mod.rs:768-796       -> vbf_meta_parse
  *   BloomFilter::clear                 src/filter/bf.rs:180-195    -> vbf_filter_clear
  *   num_elements / num_bits / num_of_hash_functions bf.rs:198-213  -> vbf_filter_num_*
@@ -57,6 +60,9 @@ extern "C" {
 
 /* `device` of a filter whose bits live in host memory (see "Residency" below). */
 #define VBF_DEVICE_HOST (-1)
+/* `device` for vbf_filter_new, _new_sized, _default, _recover, _recover_ext and _migrate: the library places the filter,
+ * round-robin over the visible devices (successive filters land on different GPUs). */
+#define VBF_DEVICE_AUTO (-2)
 
 const char* vbf_version(void);
 const char* vbf_last_error(void); /* thread-local; "" when the last call succeeded */
@@ -208,7 +214,34 @@ int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offs
                         uint64_t stride, uint64_t n, int len_prefix);
 int vbf_filter_set_dev(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
                        uint64_t n, int len_prefix, void* stream);
-/* contains over a batch (bf.rs:95-105): out[j] = 1 when every one of the k bits is set. */
+/* set over host keys, returning before the work is done (build_filter_from_entries for a
+ * device-resident filter, bf.rs:126-128, without blocking the caller).  The batch is queued on
+ * its device's worker thread, which streams it to the GPU exactly as vbf_filter_set_host does;
+ * no_of_elements += n at once.  Every later call on the filter (or a clone) first waits for the
+ * queued sets, so results are those of the synchronous call; a failure is returned by the next
+ * call on the filter.  With `release` NULL the library copies the keys before returning (the
+ * caller may reuse its buffers); otherwise it reads the caller's buffers and calls
+ * release(release_ctx) from its worker once it no longer needs them (a Rust caller hands over
+ * its packed Vec and drops it there).  Host-resident filters set synchronously (then release). */
+int vbf_filter_set_host_async(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                              uint64_t n, int len_prefix, void (*release)(void*), void* release_ctx);
+/* Wait until every queued or in-flight operation on the filter has finished (returns a queued
+ * set's failure).  vbf_filter_busy: 1 while such work is outstanding, 0 when idle, < 0 error. */
+int vbf_filter_sync(vbf_filter* f);
+int vbf_filter_busy(const vbf_filter* f);
+/* Writers of the bits through vbf_filter_words_dev (an OR/merge kernel on the caller's stream)
+ * bracket their work: vbf_filter_stream_wait makes `stream` wait for the filter's previous
+ * operations, vbf_filter_stream_record makes the work queued on `stream` so far the filter's
+ * last operation (later calls are ordered after it; the host mirror is invalidated).  A writer
+ * that skips them must synchronize its stream before the next call on the filter. */
+int vbf_filter_stream_wait(const vbf_filter* f, void* stream);
+int vbf_filter_stream_record(vbf_filter* f, void* stream);
+/* contains over a batch (bf.rs:95-105): out[j] = 1 when every one of the k bits is set.
+ * Host mirror: a device-resident filter keeps a pinned host copy of its bits, refreshed after
+ * device writes, and vbf_filter_contains_host / vbf_multi_probe_host batches of at most
+ * VBF_MIRROR_MAX_KEYS (env, default 256) keys answer from it on the CPU -- the read path's one
+ * contains per SST per get (key_range/range.rs:130,136,171) costs what it costs on a
+ * host-resident filter instead of a PCIe round trip.  Larger batches run on the GPU. */
 int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uint64_t* offsets,
                              uint64_t stride, uint64_t n, int len_prefix, uint8_t* out);
 int vbf_filter_contains_dev(const vbf_filter* f, const uint8_t* keys, const uint64_t* offsets,
@@ -231,6 +264,37 @@ int vbf_filter_clear(vbf_filter* f, vbf_filter** out);
 /* Bit-array persistence: copy the ceil(m/32) words out / in. */
 int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords);
 int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nwords);
+
+/* Host mirror mode (see contains above): OFF frees it and sends every contains to the GPU;
+ * LAZY (default, env VBF_MIRROR) fills it with one D2H on the first small contains after a
+ * device write; EAGER queues that D2H behind every device write, off the read path. */
+#define VBF_MIRROR_OFF 0
+#define VBF_MIRROR_LAZY 1
+#define VBF_MIRROR_EAGER 2
+int vbf_filter_set_mirror(vbf_filter* f, int mode);
+
+/* filter.db with the bit array persisted after the reference's 16 bytes.
+ * Layout (little-endian): the 16-byte header of vbf_filter_serialize (bf.rs:158-172), then
+ *   u32 magic "VBFW" | u32 version 2 | u32 m | u32 nwords | u64 entries | u64 checksum | words
+ * The reference reads exactly 16 bytes (fs/mod.rs:768-796), so the file stays readable by it.
+ * The words are those recover_meta + build_filter_from_entries (range.rs:117-128) would rebuild:
+ * a filter of m = num_bits(n_stored, p) bits (bf.rs:144-147) holding the SST's `entries` keys.
+ *
+ * vbf_filter_serialize_ext: `entries` = the SST's data.db entry count, or VBF_EXT_NONE for the
+ * reference's 16 bytes alone.  When the filter's own m equals that recovery m (a compaction-built
+ * filter, sized from its table's entries: sized.rs:192-193) its words are written; otherwise
+ * (a memtable-born filter, sized from the write-buffer capacity: mem.rs:188-191) the recovery-
+ * shaped words are built from `keys` (the SST's `entries` keys, layout as for set; on the CPU for
+ * a host-resident filter, on its GPU otherwise), and with no keys only the 16 bytes are written.
+ * *len = bytes needed; buf NULL is a size query; cap < *len is VBF_EINVAL.
+ * vbf_filter_recover_ext: vbf_filter_recover, then, when the extension is present, intact
+ * (checksum) and of the recovered m, loads its words and sets no_of_elements = n + entries
+ * (what the rebuild leaves), *restored = 1: the caller skips the rebuild.  Otherwise
+ * *restored = 0 and the caller rebuilds as the reference does. */
+#define VBF_EXT_NONE UINT64_MAX
+int vbf_filter_serialize_ext(const vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                             uint64_t entries, int len_prefix, uint8_t* buf, uint64_t cap, uint64_t* len);
+int vbf_filter_recover_ext(const uint8_t* bytes, uint64_t len, int device, vbf_filter** out, int* restored);
 
 /* Synthetic data.db (bench / tests): n entries whose keys are vbf_gen_fixed_dev's, value offset
  * (u32)j, created_at 1720785462000 + j ms, tombstone j % 97 == 0, blocked as

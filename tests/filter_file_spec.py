@@ -1,5 +1,7 @@
 """`filter.db` with the bit array persisted after the reference's 16-byte header (SURVEY.md
-8(f) row 1).
+8(f) row 1) -- an independent Python restatement of the layout that libvbf writes and reads
+(vbf_filter_serialize_ext / vbf_filter_recover_ext, include/vbf.h); the tests check the C ABI's
+bytes against it.
 
 velarixdb writes only `u32 k | u32 n | f64 p` (src/filter/bf.rs:158-172) and rebuilds the bits
 from data.db on the first read after a restart (src/key_range/range.rs:117-128), with m
@@ -41,13 +43,14 @@ def fast_checksum(words):
 
 
 def encode(k, n, p, m=None, words=None, entries=None):
-    """`entries`: the SST's data.db entry count (defaults to n, which is exact for a filter built
-    from its table's entries, as compaction builds them: sized.rs:192-193)."""
+    """`entries`: the SST's data.db entry count, required with `words` (only the writer that
+    knows the SST can give it: a memtable filter counts sets, not entries, mem.rs:209-211)."""
     out = HEADER.pack(k & 0xFFFFFFFF, n & 0xFFFFFFFF, p)
     if words is not None:
+        if entries is None:
+            raise ValueError("persisted words need the SST's entry count")
         w = np.ascontiguousarray(words, dtype="<u4")
-        ent = n if entries is None else entries
-        out += EXT.pack(MAGIC, VERSION, m, w.size, ent, fast_checksum(w)) + w.tobytes()
+        out += EXT.pack(MAGIC, VERSION, m, w.size, entries, fast_checksum(w)) + w.tobytes()
     return out
 
 

@@ -131,28 +131,130 @@ def test_product_never_imports_oracle():
 
 
 def test_filter_file_extension_roundtrip():
-    """filter.db with persisted bits: the first 16 bytes stay the reference's format."""
+    """filter.db with persisted bits (the layout spec, tests/filter_file_spec.py): the first 16
+    bytes stay the reference's format."""
     import numpy as np
-    from velarixdb_amd import filter_file
+    from tests import filter_file_spec as ff
     w = np.arange(1, 1074, dtype=np.uint32) * np.uint32(2654435761)
-    raw = filter_file.encode(19, 1791, 1e-4, 34333, w, entries=2844)
+    raw = ff.encode(19, 1791, 1e-4, 34333, w, entries=2844)
     assert raw[:16] == struct.pack("<IId", 19, 1791, 1e-4)
-    k, n, p, m, words, ent = filter_file.decode(raw)
+    k, n, p, m, words, ent = ff.decode(raw)
     assert (k, n, p, m, ent) == (19, 1791, 1e-4, 34333, 2844) and np.array_equal(words, w)
-    assert filter_file.decode(filter_file.encode(19, 1791, 1e-4, 34333, w))[5] == 1791  # default: n
+    with pytest.raises(ValueError):  # ADVICE r02: only the SST's writer knows the entry count
+        ff.encode(19, 1791, 1e-4, 34333, w)
     # corrupted body -> ignored (caller rebuilds, as the reference does)
     bad = bytearray(raw)
     bad[-1] ^= 0xFF
-    assert filter_file.decode(bytes(bad))[3:] == (None, None, None)
+    assert ff.decode(bytes(bad))[3:] == (None, None, None)
     # a version-1 extension (no entry count) is ignored too
     v1 = bytearray(raw)
     v1[20:24] = struct.pack("<I", 1)
-    assert filter_file.decode(bytes(v1))[3:] == (None, None, None)
+    assert ff.decode(bytes(v1))[3:] == (None, None, None)
     # the reference's own 16-byte files decode without words
     ref = open(os.path.join(ROOT, "tests/golden/sst_fixtures/sstable_1720785462309/filter.db"), "rb").read()
-    assert filter_file.decode(ref) == (19, 1791, 1e-4, None, None, None)
+    assert ff.decode(ref) == (19, 1791, 1e-4, None, None, None)
     with pytest.raises(EOFError):
-        filter_file.decode(ref[:12])
+        ff.decode(ref[:12])
+
+
+def _recover_raw(raw, offset=0):
+    """vbf_filter_recover_ext on host residency from `raw` placed at `offset` in a buffer."""
+    import ctypes
+    import numpy as np
+    from velarixdb_amd import BloomFilter
+    from velarixdb_amd._lib import VBF_DEVICE_HOST, call
+    buf = np.zeros(len(raw) + offset, dtype=np.uint8)
+    buf[offset:] = np.frombuffer(raw, dtype=np.uint8)
+    h, restored = ctypes.c_void_p(), ctypes.c_int(-1)
+    call("vbf_filter_recover_ext", buf.ctypes.data + offset, len(raw), VBF_DEVICE_HOST, ctypes.byref(h),
+         ctypes.byref(restored))
+    return BloomFilter(_handle=h), bool(restored.value)
+
+
+def test_serialize_ext_compaction_filter(ora):
+    """SURVEY 8(f) row 1 through the C ABI, host residency (no GPU): a compaction-built filter
+    (sized from its table's entries, sized.rs:192-193) persists its own words; recovery restores
+    them with no_of_elements = n + entries, as recover_meta + rebuild leave it (range.rs:117-128),
+    and the bytes equal the layout spec's."""
+    import numpy as np
+    from tests import filter_file_spec as ff
+    from velarixdb_amd import BloomFilter
+    from velarixdb_amd.keys import pack
+    keys = [b"k%06d" % i for i in range(17064)]
+    bf = BloomFilter(0.01, len(keys), device="host")
+    bf.build_filter_from_entries(keys)
+    raw = bf.serialize_ext(sst_entries=len(keys))
+    w = bf.words()
+    assert raw == ff.encode(9, 17064, 0.01, 163559, w, entries=17064)
+    assert raw[:16] == bf.serialize() == struct.pack("<IId", 9, 17064, 0.01)
+    assert np.array_equal(w, ora.build_words(pack(keys), 163559, 9))
+    assert bf.serialize_ext() == raw[:16]  # no entry count: the reference's file only
+    for off in (0, 1, 3):  # unaligned bodies
+        r, restored = _recover_raw(raw, off)
+        assert restored and np.array_equal(r.words(), w)
+        assert r.no_of_elements == 2 * 17064 and r.num_bits() == 163559 and r.no_of_hash_func == 9
+    # the reference's rebuild gives the same bits and serialize() bytes
+    rb, restored = _recover_raw(raw[:16])
+    assert not restored and rb.no_of_elements == 17064 and not rb.words().any()
+    rb.build_filter_from_entries(keys)
+    assert np.array_equal(rb.words(), w) and rb.serialize() == r.serialize()
+    # a damaged or foreign extension is ignored: the caller rebuilds
+    for i in (16, 20, 24, 28, 40, len(raw) - 1):
+        bad = bytearray(raw)
+        bad[i] ^= 0x5A
+        r2, restored = _recover_raw(bytes(bad))
+        assert not restored and r2.no_of_elements == 17064 and not r2.words().any(), i
+    r3, restored = _recover_raw(raw[:-4])
+    assert not restored
+
+
+def test_serialize_ext_memtable_filter(ora, tmp_path):
+    """A memtable-born filter (sized from the write buffer, mem.rs:188-191: 512 entries, m = 9815)
+    holding 300 keys recovers with m' = num_bits(300, p) (bf.rs:144-147): its own words cannot be
+    reused, so the writer passes the SST's keys and the recovery-shaped words are built from them
+    -- equal to the reference's rebuild.  Without keys only the 16 bytes are written."""
+    import numpy as np
+    from velarixdb_amd import BloomFilter, num_bits
+    from velarixdb_amd.keys import pack
+    keys = [b"mem%05d" % i for i in range(300)]
+    mem = BloomFilter(1e-4, 512, device="host")
+    mem.set_many(keys)
+    assert mem.num_bits() == 9815 and num_bits(300, 1e-4) != 9815
+    assert mem.serialize_ext(sst_entries=300) == mem.serialize()  # no keys: nothing to persist
+    raw = mem.serialize_ext(sst_entries=300, sst_keys=keys)
+    m2 = num_bits(300, 1e-4)
+    r, restored = _recover_raw(raw)
+    assert restored and r.num_bits() == m2 and r.no_of_elements == 600
+    assert np.array_equal(r.words(), ora.build_words(pack(keys), m2, 19))
+    # through write / recover_from_sst-style recover_meta
+    mem.write(tmp_path, sst_entries=300, sst_keys=keys)
+    f = BloomFilter.default(device="host")
+    f.file_path = str(tmp_path / "filter.db")
+    assert f.recover_meta() is True and np.array_equal(f.words(), r.words())
+    g = BloomFilter.default(device="host")
+    g.file_path = f.file_path
+    assert g.recover_meta(load_bits=False) is False
+    g.build_filter_from_entries(keys)
+    assert np.array_equal(g.words(), r.words()) and g.serialize() == f.serialize()
+    with pytest.raises(ValueError):
+        mem.serialize_ext(sst_entries=299, sst_keys=keys)
+
+
+def test_serialize_ext_size_query_and_errors():
+    import ctypes
+    from velarixdb_amd import BloomFilter
+    from velarixdb_amd._lib import VBF_EINVAL, lib
+    bf = BloomFilter(0.01, 1000, device="host")
+    bf.set_many([b"a%d" % i for i in range(1000)])  # stored n = 1000: the recovery m is this m
+    n = ctypes.c_uint64()
+    assert lib.vbf_filter_serialize_ext(bf._h, None, None, 0, 1000, 1, None, 0, ctypes.byref(n)) == 0
+    assert n.value == 16 + 32 + 4 * ((bf.num_bits() + 31) // 32)
+    buf = (ctypes.c_uint8 * 8)()
+    assert lib.vbf_filter_serialize_ext(bf._h, None, None, 0, 1000, 1, buf, 8, ctypes.byref(n)) == VBF_EINVAL
+    # the reference's fixtures (16 bytes) recover unchanged
+    raw = open(os.path.join(ROOT, "tests/golden/sst_fixtures/sstable_1720785462309/filter.db"), "rb").read()
+    r, restored = _recover_raw(raw)
+    assert not restored and (r.no_of_hash_func, r.no_of_elements, r.num_bits()) == (19, 1791, 34333)
 
 
 def test_shard_build_argument_checks():

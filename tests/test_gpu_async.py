@@ -1,0 +1,266 @@
+"""Round-3 boundary features on the GPU: the host mirror of device-resident filters, the
+asynchronous host-key set, device placement, external writers, and residency races.
+
+* Host mirror: the reference's read path calls contains once per in-range SST
+  per get (key_range/range.rs:130,136,171).  A compaction-built or recovered filter lives in HBM;
+  small contains batches answer on the CPU from a pinned host copy refreshed after device writes,
+  and must give the oracle's answers even right after an asynchronous set_dev on a side stream.
+* set_host_async: build_filter_from_entries for a device-resident filter
+  returns before the GPU work is done, so the serial compaction loop (compactors/sized.rs:170-200)
+  keeps merging while the GPUs build; later calls wait for it, and the words equal the oracle.
+* a migrate racing set/contains on a clone must neither crash nor lose bits.
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SLEEP_CYCLES = 40_000_000  # ~17 ms of a spinning kernel ahead of the set_dev
+
+
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _side_stream_set(vbf, bf, n, seed, L=16):
+    s = torch.cuda.Stream()
+    keys = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+    sp = ctypes.c_void_p(s.cuda_stream)
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(SLEEP_CYCLES)
+    vbf._lib.call("vbf_gen_fixed_dev", seed, 0, n, L, _vp(keys), sp)
+    bf.set_dev(_vp(keys), None, L, n, 1, sp)
+    return s, keys
+
+
+def _oracle_words(ora, seed, n, m, k, L=16):
+    from velarixdb_amd.keys import HostBatch
+    return ora.build_words(HostBatch(ora.gen_fixed(seed, 0, n, L), None, L, n, 1), m, k, threads=8)
+
+
+@pytest.mark.parametrize("mode", ["lazy", "eager"])
+def test_mirror_answers_after_async_set_dev(vbf, ora, mode):
+    """Single-key and small-batch contains on a device filter, issued with no synchronisation
+    right after a set_dev queued behind a spinning kernel on a side stream: every answer equals
+    the oracle's probe of the oracle's words (positives and negatives)."""
+    from velarixdb_amd.keys import HostBatch
+    n, seed = 2_000_000, 0x5EED0C01
+    bf = vbf.BloomFilter(0.01, n)
+    bf.set_mirror(mode)
+    s, keys = _side_stream_set(vbf, bf, n, seed)
+    pos = ora.gen_fixed(seed, 0, 200, 16)
+    neg = ora.gen_fixed(seed ^ 0xFFFF, 0, 200, 16)
+    got_single = [bf.contains(bytes(pos[i * 16:(i + 1) * 16])) for i in range(50)]
+    got_pos = bf.contains_batch(HostBatch(pos, None, 16, 200, 1))
+    got_neg = bf.contains_batch(HostBatch(neg, None, 16, 200, 1))
+    want_w = _oracle_words(ora, seed, n, bf.num_bits(), bf.no_of_hash_func)
+    assert all(got_single) and got_pos.all()
+    want_neg = ora.probe(HostBatch(neg, None, 16, 200, 1), bf.num_bits(), bf.no_of_hash_func, want_w).astype(bool)
+    assert np.array_equal(got_neg, want_neg)
+    assert np.array_equal(bf.words(), want_w)
+    # a second write invalidates the mirror: new keys are found through it too
+    more = ora.gen_fixed(seed + 1, 0, 100, 16)
+    bf.set_many(HostBatch(more, None, 16, 100, 1))
+    assert bf.contains_batch(HostBatch(more, None, 16, 100, 1)).all()
+    # mirror off: the same answers through the staged GPU probe
+    bf.set_mirror("off")
+    assert np.array_equal(bf.contains_batch(HostBatch(neg, None, 16, 200, 1)), got_neg)
+    del keys, s
+
+
+def test_mirror_after_clear_load_and_rebuild(vbf, ora, golden):
+    """Every device write path refreshes or invalidates the mirror: clear, load_words, the
+    data.db rebuild (range.rs:117-128) and a restore from persisted bits."""
+    import os
+    import hashlib
+    from conftest import GOLDEN
+    from velarixdb_amd.keys import pack
+    keys = [b"mk%05d" % i for i in range(3000)]
+    bf = vbf.BloomFilter(1e-4, 3000)
+    bf.set_many(keys)
+    assert bf.contains(keys[7])
+    bf.clear()
+    assert not bf.contains(keys[7]) and not bf.words().any()
+    w = ora.build_words(pack(keys), bf.num_bits(), bf.no_of_hash_func)
+    bf.load_words(w)
+    assert bf.contains(keys[7]) and np.array_equal(bf.words(), w)
+    # fixture SST rebuild, then the probe of its smallest key answers from the mirror
+    sst = os.path.join(GOLDEN, "sst_fixtures", "sstable_1720785462309")
+    want = golden("sst_fixtures")["ssts"][0]
+    f = vbf.BloomFilter.default()
+    f.file_path = os.path.join(sst, "filter.db")
+    f.recover_meta()
+    from tests_util import parse_data_db
+    ks = parse_data_db(os.path.join(sst, "data.db"))
+    assert not f.contains(ks[0])  # mirror of the zeroed recovered filter
+    f.rebuild_from_sst(*vbf.sst.read_sst_files(sst))
+    assert f.contains(ks[0]) and f.contains(ks[-1])
+    assert hashlib.sha256(f.words().astype("<u4").tobytes()).hexdigest() == want["sha256"]
+    negs = [b"zz%05d" % i for i in range(5000)]
+    hits = sum(int(f.contains_many(negs[i:i + 250]).sum()) for i in range(0, 5000, 250))  # mirror batches
+    assert hits == want["neg_hits_zz5000"]
+
+
+def test_multi_probe_small_batch_from_mirrors(vbf, ora):
+    """vbf_multi_probe_host with a get-sized batch answers from the filters' mirrors: equal to
+    the GPU path (mirrors off) and to the range test + oracle probe, keys in and out of range."""
+    from velarixdb_amd.key_range import SstRange, candidates
+    from velarixdb_amd.keys import pack
+    rng = np.random.default_rng(5)
+    ranges = []
+    for s in range(6):
+        ks = sorted({bytes(rng.integers(97, 123, size=int(rng.integers(3, 12)), dtype=np.uint8)) for _ in range(2000)})
+        f = vbf.BloomFilter(1e-3 if s % 2 else 1e-4, len(ks))
+        f.set_many(ks)
+        ranges.append((SstRange(ks[0], ks[-1], f), ks))
+    probe = [ks[i] for _, ks in ranges for i in (0, 5, len(ks) - 1)]
+    probe += [bytes(rng.integers(97, 123, size=6, dtype=np.uint8)) for _ in range(60)]
+    rs = [r for r, _ in ranges]
+    got = candidates(probe, rs)  # 78 keys: the mirror path
+    for r in rs:
+        r.filter.set_mirror("off")
+    assert np.array_equal(candidates(probe, rs), got)  # the GPU path
+    for s, (r, ks) in enumerate(ranges):
+        w = r.filter.words()
+        inr = np.array([r.smallest_key <= k <= r.biggest_key for k in probe])
+        hit = ora.probe(pack(probe), r.filter.num_bits(), r.filter.no_of_hash_func, w).astype(bool)
+        assert np.array_equal(got[:, s], inr & hit), s
+
+
+def test_set_host_async_returns_before_the_build(vbf, ora):
+    """set_many_async returns while the build is still running (busy), the next call waits for
+    it, and the words equal the oracle's.  The library copied the keys: the caller's buffer is
+    overwritten right after the call without effect."""
+    from velarixdb_amd.keys import HostBatch
+    n, seed = 20_000_000, 0x5EED0C02
+    host = ora.gen_fixed(seed, 0, n, 16)
+    bf = vbf.BloomFilter(0.01, n)
+    bf.set_many_async(HostBatch(host, None, 16, n, 1))
+    assert bf.busy(), "set_host_async waited for its GPU work"
+    assert bf.no_of_elements == n
+    saved = host.copy()
+    host[:] = 0  # the library works from its own copy
+    assert bf.contains(bytes(saved[:16]))  # waits for the queued set
+    assert not bf.busy()
+    assert np.array_equal(bf.words(), _oracle_words(ora, seed, n, bf.num_bits(), bf.no_of_hash_func))
+
+
+def test_set_host_async_release_callback_and_order(vbf, ora):
+    """The zero-copy form: the library reads the caller's buffer and calls release(ctx) from
+    its worker when done (a Rust caller drops its packed Vec there).  Two queued batches and a
+    clone's set land in submission order; sync() waits for all."""
+    from velarixdb_amd._lib import call
+    from velarixdb_amd.keys import HostBatch
+    n, seed = 8_000_000, 0x5EED0C03
+    a = ora.gen_fixed(seed, 0, n, 16)
+    b = ora.gen_fixed(seed, n, n, 16)
+    released = []
+    done = threading.Event()
+    CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+    def rel(ctx):
+        released.append(ctx)
+        if len(released) == 2:
+            done.set()
+
+    cb = CB(rel)
+    bf = vbf.BloomFilter(0.01, 2 * n)
+    call("vbf_filter_set_host_async", bf._h, a.ctypes.data, None, 16, n, 1, ctypes.cast(cb, ctypes.c_void_p), 11)
+    c = bf.clone()
+    call("vbf_filter_set_host_async", c._h, b.ctypes.data, None, 16, n, 1, ctypes.cast(cb, ctypes.c_void_p), 22)
+    assert bf.busy()
+    bf.sync()
+    assert done.wait(5) and released == [11, 22]
+    assert not c.busy()
+    want = _oracle_words(ora, seed, 2 * n, bf.num_bits(), bf.no_of_hash_func)
+    assert np.array_equal(c.words(), want)
+    assert bf.no_of_elements == n and c.no_of_elements == 2 * n  # counters per handle (bf.rs:248)
+    # host-resident filters set at once and release immediately
+    h = vbf.BloomFilter(0.01, 1000, device="host")
+    small = HostBatch(a[:16000], None, 16, 1000, 1)
+    call("vbf_filter_set_host_async", h._h, small.data.ctypes.data, None, 16, 1000, 1,
+         ctypes.cast(cb, ctypes.c_void_p), 33)
+    assert released[-1] == 33 and not h.busy()
+
+
+def test_auto_placement_and_fanout(vbf, ora):
+    """VBF_DEVICE_AUTO: filters land round-robin on the visible GPUs (one here); several filters
+    built asynchronously from one thread, as a serial compaction loop would, all bit-exact."""
+    from velarixdb_amd.keys import HostBatch
+    ndev = vbf.device_count()
+    fs = []
+    for t in range(4):
+        n = 1_000_000 + 250_000 * t
+        f = vbf.BloomFilter(0.001, n, device="auto")
+        assert 0 <= f.device < ndev
+        host = ora.gen_fixed(0x5EED0D00 + t, 0, n, 16)
+        f.set_many_async(HostBatch(host, None, 16, n, 1))
+        fs.append((f, n))
+    devs = [f.device for f, _ in fs]
+    assert devs == [(devs[0] + i) % ndev for i in range(4)]
+    for t, (f, n) in enumerate(fs):
+        assert np.array_equal(f.words(), _oracle_words(ora, 0x5EED0D00 + t, n, f.num_bits(), f.no_of_hash_func))
+
+
+def test_external_writer_stream_record(vbf, ora):
+    """A kernel writing the bits through words_dev_ptr (here the OR of a second filter) bracketed
+    by stream_wait / stream_record: later host calls (mirror contains, words) see its result."""
+    from velarixdb_amd._lib import call
+    from velarixdb_amd.keys import pack
+    ka = [b"a%05d" % i for i in range(4000)]
+    kb = [b"b%05d" % i for i in range(4000)]
+    fa = vbf.BloomFilter.sized(200_000, 7)
+    fb = vbf.BloomFilter.sized(200_000, 7)
+    fa.set_many(ka)
+    fb.set_many(kb)
+    assert not fa.contains_many(kb[:100]).all()
+    s = torch.cuda.Stream()
+    sp = ctypes.c_void_p(s.cuda_stream)
+    call("vbf_filter_stream_wait", fa._h, sp)
+    call("vbf_filter_stream_wait", fb._h, sp)
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(SLEEP_CYCLES)
+    call("vbf_or_words_dev", ctypes.c_void_p(fa.words_dev_ptr()), ctypes.c_void_p(fb.words_dev_ptr()),
+         fa.num_words(), sp)
+    call("vbf_filter_stream_record", fa._h, sp)
+    assert fa.contains_many(kb[:100]).all() and fa.contains_many(ka[:100]).all()
+    assert np.array_equal(fa.words(), ora.build_words(pack(ka + kb), 200_000, 7))
+
+
+def test_migrate_races_set_and_contains_on_a_clone(vbf, ora):
+    """residency is read under the filter's lock.  One thread moves the
+    bits between host and GPU while another sets and probes through a clone; no crash, every
+    key set is found, and the final words equal the oracle's."""
+    from velarixdb_amd import HOST
+    from velarixdb_amd.keys import pack
+    keys = [b"race%06d" % i for i in range(20000)]
+    bf = vbf.BloomFilter(1e-3, len(keys), device=HOST)
+    c = bf.clone()
+    stop = threading.Event()
+    errs = []
+
+    def mover():
+        try:
+            i = 0
+            while not stop.is_set():
+                bf.migrate(0 if i % 2 == 0 else HOST)
+                i += 1
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = threading.Thread(target=mover)
+    th.start()
+    try:
+        for i in range(0, len(keys), 500):
+            c.set_many(keys[i:i + 500])
+            assert c.contains_many(keys[:i + 500]).all()
+            assert c.contains(keys[i])
+    finally:
+        stop.set()
+        th.join()
+    assert not errs, errs
+    assert np.array_equal(bf.words(), ora.build_words(pack(keys), bf.num_bits(), bf.no_of_hash_func))

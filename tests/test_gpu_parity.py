@@ -359,7 +359,7 @@ def test_filter_db_persisted_bits(vbf, tmp_path):
     keys = [b"k%06d" % i for i in range(17064)]
     bf = BloomFilter(0.01, len(keys))  # compactors/sized.rs:192 sizing
     bf.build_filter_from_entries(keys)
-    bf.write(tmp_path)
+    bf.write(tmp_path, sst_entries=len(keys))
     r = BloomFilter.default()
     r.file_path = bf.file_path
     assert r.recover_meta() is True
@@ -368,15 +368,22 @@ def test_filter_db_persisted_bits(vbf, tmp_path):
     assert rebuilt.recover_meta(load_bits=False) is False
     rebuilt.build_filter_from_entries(keys)  # what range.rs:117-128 does
     assert np.array_equal(r.words(), rebuilt.words())
-    # memtable-born: sized for 512 entries, holds 300 -> stored n = 300, m' != m
+    # memtable-born: sized for 512 entries, holds 300 -> stored n = 300, m' != m: its own words
+    # cannot be restored; with the SST's keys the writer persists the recovery-shaped words
     mem = BloomFilter(1e-4, 512)
     mem.set_many(keys[:300])
     d2 = tmp_path / "mem"
     d2.mkdir()
-    mem.write(d2)
+    mem.write(d2, sst_entries=300)
     r2 = BloomFilter.default()
     r2.file_path = mem.file_path
     assert r2.recover_meta() is False and not r2.words().any()
+    mem.write(d2, sst_entries=300, sst_keys=keys[:300])
+    r3 = BloomFilter.default()
+    r3.file_path = mem.file_path
+    assert r3.recover_meta() is True and r3.no_of_elements == 600
+    r2.build_filter_from_entries(keys[:300])  # what range.rs:117-128 does
+    assert np.array_equal(r3.words(), r2.words()) and r3.serialize() == r2.serialize()
 
 
 def test_product_library_ignores_ablation_env(vbf, tmp_path):

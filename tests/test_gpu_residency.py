@@ -227,7 +227,7 @@ def test_restored_bits_match_rebuild_count(vbf, tmp_path):
     ent = vbf.sst.load_entries_from_dir(d)
     f = BloomFilter(0.01, len(ent))  # sized.rs:192-193 sizing
     f.set_many(ent.key_list())
-    f.write(d)
+    f.write(d, sst_entries=len(ent))
     a, b = BloomFilter.default(), BloomFilter.default()
     assert a.recover_from_sst_dir(d) is True
     b.file_path = os.path.join(d, "filter.db")

@@ -67,7 +67,7 @@ def test_fixture_rebuild_matches_golden(vbf, golden, tmp_path):
         p = float.fromhex(want[name]["p"])
         f = vbf.BloomFilter(p, len(ent))
         f.set_many(ent.key_list())
-        f.write(d)
+        f.write(d, sst_entries=len(ent))
         f2 = vbf.BloomFilter.default()
         assert f2.recover_from_sst_dir(d) is True
         assert np.array_equal(f2.words(), f.words())

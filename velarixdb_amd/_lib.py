@@ -17,6 +17,9 @@ VBF_ENOMEM = -3
 VBF_ENODEV = -4
 VBF_EDIVZERO = -5
 VBF_DEVICE_HOST = -1
+VBF_DEVICE_AUTO = -2  # the library places the filter (round-robin over the devices)
+VBF_MIRROR_OFF, VBF_MIRROR_LAZY, VBF_MIRROR_EAGER = 0, 1, 2
+VBF_EXT_NONE = 0xFFFFFFFFFFFFFFFF  # vbf_filter_serialize_ext: the reference's 16 bytes only
 
 VBF_BUILD_AUTO = 0
 VBF_BUILD_ATOMIC = 1
@@ -67,6 +70,14 @@ SIGNATURES = {
     "vbf_filter_free": (None, [_vp]),
     "vbf_filter_set_host": (_int, [_vp, _vp, _vp, _u64, _u64, _int]),
     "vbf_filter_set_dev": (_int, [_vp, _vp, _vp, _u64, _u64, _int, _vp]),
+    "vbf_filter_set_host_async": (_int, [_vp, _vp, _vp, _u64, _u64, _int, _vp, _vp]),
+    "vbf_filter_sync": (_int, [_vp]),
+    "vbf_filter_busy": (_int, [_vp]),
+    "vbf_filter_stream_wait": (_int, [_vp, _vp]),
+    "vbf_filter_stream_record": (_int, [_vp, _vp]),
+    "vbf_filter_set_mirror": (_int, [_vp, _int]),
+    "vbf_filter_serialize_ext": (_int, [_vp, _vp, _vp, _u64, _u64, _int, _vp, _u64, ctypes.POINTER(_u64)]),
+    "vbf_filter_recover_ext": (_int, [_vp, _u64, _int, ctypes.POINTER(_vp), ctypes.POINTER(_int)]),
     "vbf_filter_contains_host": (_int, [_vp, _vp, _vp, _u64, _u64, _int, _vp]),
     "vbf_filter_contains_dev": (_int, [_vp, _vp, _vp, _u64, _u64, _int, _vp, _vp]),
     "vbf_filter_num_bits": (_u32, [_vp]),

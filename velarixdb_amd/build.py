@@ -37,10 +37,17 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     os.makedirs(objdir, exist_ok=True)
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++20", "-fPIC", "-Wall"] + ["-D" + d for d in defines]
     procs, objs = [], []
+    # an object is current when newer than its source, every header and this script
+    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hpp")] + [
+        os.path.join(HERE, "..", "include", "vbf.h"), __file__]
+    t_hdr = max(os.path.getmtime(h) for h in hdrs if os.path.exists(h))
     for s in SOURCES:
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
         objs.append(obj)
-        cmd = [_hipcc()] + flags + ["-c", os.path.join(CSRC, s), "-o", obj]
+        src = os.path.join(CSRC, s)
+        if (not force and os.path.exists(obj) and os.path.getmtime(obj) > max(t_hdr, os.path.getmtime(src))):
+            continue
+        cmd = [_hipcc()] + flags + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((s, subprocess.Popen(cmd, cwd=CSRC)))

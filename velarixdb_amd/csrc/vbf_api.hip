@@ -22,6 +22,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../../include/vbf.h"
 #include "sip13.hpp"
 #include "vbf_kernels.hpp"
@@ -271,7 +273,12 @@ constexpr uint64_t kChunkBytes = 64ull << 20;
 class CopyPool {
   public:
     static CopyPool& get() {
-        static CopyPool* p = new CopyPool();  // never destroyed: workers outlive static teardown
+        static std::mutex mu;
+        static CopyPool* p = nullptr;  // never destroyed: workers outlive static teardown
+        std::lock_guard<std::mutex> lk(mu);
+        // a forked child (e.g. a multiprocessing fork) inherits the pool but not its threads:
+        // it gets a pool of its own
+        if (!p || p->pid_ != getpid()) p = new CopyPool();
         return *p;
     }
     unsigned threads() const { return nt_; }
@@ -295,7 +302,7 @@ class CopyPool {
     }
 
   private:
-    CopyPool() {
+    CopyPool() : pid_(getpid()) {
         const char* e = getenv("VBF_COPY_THREADS");
         const unsigned hw = std::thread::hardware_concurrency();
         const int v = e ? atoi(e) : (int)std::min(8u, hw ? hw : 1u);
@@ -318,6 +325,7 @@ class CopyPool {
             }
         }
     }
+    const pid_t pid_;
     unsigned nt_ = 1;
     std::mutex call_mu_, mu_;
     std::condition_variable cv_, done_cv_;
@@ -559,7 +567,28 @@ struct Storage {
     hipEvent_t last = nullptr;
     bool pending = false;
     std::mutex mu;  // the reference's Mutex<BitVec>
+    // Asynchronous set_host jobs (vbf_filter_set_host_async) queued on the device's worker and
+    // not yet run.  Every other call on the filter first waits for them (storage_drain), so calls
+    // stay ordered as the reference's Mutex orders them; a failed job's status is reported by the
+    // next call that drains.
+    uint64_t jobs_queued = 0, jobs_done = 0;
+    std::condition_variable jobs_cv;
+    int async_rc = VBF_OK;
+    std::string async_msg;
+    // Host mirror of d_words (device-resident filters only): a pinned copy that answers
+    // single-key contains on the CPU, as the reference's read path calls it once per SST per get
+    // (key_range/range.rs:130,136,171).  Valid while no device write happened since it was
+    // filled; filled lazily by the first small contains (one D2H), or queued right after every
+    // device write in VBF_MIRROR_EAGER mode.
+    int mirror_mode = -1;  // -1: the process default (VBF_MIRROR, default lazy)
+    uint32_t* mirror = nullptr;
+    bool mirror_ok = false;
     bool host() const { return device == VBF_DEVICE_HOST; }
+    void free_mirror() {
+        if (mirror) (void)hipHostFree(mirror);
+        mirror = nullptr;
+        mirror_ok = false;
+    }
     ~Storage() {
         if (d_words) {
             int prev = -1;
@@ -569,9 +598,42 @@ struct Storage {
             (void)hipFree(d_words);
             if (prev >= 0) (void)hipSetDevice(prev);
         }
+        free_mirror();
         if (last) (void)hipEventDestroy(last);
     }
 };
+
+// Caller holds `lk` on s.mu: waits until every asynchronous set_host job queued on the filter
+// has run (the worker takes s.mu to run one, the wait releases it), then reports a failed job.
+int storage_drain(Storage& s, std::unique_lock<std::mutex>& lk) {
+    s.jobs_cv.wait(lk, [&] { return s.jobs_done == s.jobs_queued; });
+    if (s.async_rc != VBF_OK) {
+        const int rc = s.async_rc;
+        const std::string m = s.async_msg;
+        s.async_rc = VBF_OK;
+        s.async_msg.clear();
+        return fail(rc, "an earlier asynchronous set on this filter failed: %s", m.c_str());
+    }
+    return VBF_OK;
+}
+
+int mirror_default() {
+    static const int v = [] {
+        const char* e = getenv("VBF_MIRROR");
+        return e ? std::max(0, std::min(2, atoi(e))) : (int)VBF_MIRROR_LAZY;
+    }();
+    return v;
+}
+inline int mirror_mode(const Storage& s) { return s.mirror_mode < 0 ? mirror_default() : s.mirror_mode; }
+// contains_host batches of at most this many keys answer from the mirror (~0.1 us per key on
+// one core, against ~27 us for the staged GPU round trip)
+uint64_t mirror_max_keys() {
+    static const uint64_t v = [] {
+        const char* e = getenv("VBF_MIRROR_MAX_KEYS");
+        return e ? (uint64_t)strtoull(e, nullptr, 10) : (uint64_t)256;
+    }();
+    return v;
+}
 
 // Caller holds s.mu.  The stream `st` (any, including the legacy NULL stream) waits for the
 // filter's last asynchronous operation.
@@ -593,6 +655,18 @@ int storage_sync(Storage& s) {
         s.pending = false;
     }
     return VBF_OK;
+}
+
+// Caller holds s.mu, on s.device: a device write was just queued on `st` (and marked).  The
+// mirror is stale; in eager mode its refresh is queued behind the write on the same stream, so
+// it is valid once the filter's last event completes (every host reader syncs that first).
+int mirror_after_write(Storage& s, hipStream_t st) {
+    s.mirror_ok = false;
+    if (mirror_mode(s) != VBF_MIRROR_EAGER || !s.nwords) return VBF_OK;
+    if (!s.mirror) HIP_TRY(hipHostMalloc((void**)&s.mirror, s.nwords * 4, hipHostMallocDefault));
+    HIP_TRY(hipMemcpyAsync(s.mirror, s.d_words, s.nwords * 4, hipMemcpyDeviceToHost, st));
+    s.mirror_ok = true;
+    return storage_mark(s, st);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -633,25 +707,23 @@ inline void host_key(const uint8_t* keys, const uint64_t* offsets, uint64_t stri
 }
 
 // bf.rs:84-92 per key (the caller counts the elements).
-void host_set(Storage& s, uint32_t k, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+void host_set(uint32_t* w, uint32_t m, uint32_t k, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
               uint64_t n, bool lp) {
-    uint32_t* w = s.h_words.data();
     for (uint64_t j = 0; j < n; ++j) {
         const uint8_t* kp;
         uint64_t len;
         host_key(keys, offsets, stride, j, &kp, &len);
         const vbf::Prefix p = host_prefix(kp, len, lp);
         for (uint32_t i = 0; i < k; ++i) {
-            const uint32_t idx = (uint32_t)(vbf::prefix_hash(p, i) % (uint64_t)s.m);
+            const uint32_t idx = (uint32_t)(vbf::prefix_hash(p, i) % (uint64_t)m);
             w[idx >> 5] |= 1u << (idx & 31);
         }
     }
 }
 
 // bf.rs:95-105 per key: early exit on the first clear bit; k == 0 answers true.
-void host_contains(const Storage& s, uint32_t k, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
-                   uint64_t n, bool lp, uint8_t* out) {
-    const uint32_t* w = s.h_words.data();
+void host_contains(const uint32_t* w, uint32_t m, uint32_t k, const uint8_t* keys, const uint64_t* offsets,
+                   uint64_t stride, uint64_t n, bool lp, uint8_t* out) {
     for (uint64_t j = 0; j < n; ++j) {
         const uint8_t* kp;
         uint64_t len;
@@ -659,7 +731,7 @@ void host_contains(const Storage& s, uint32_t k, const uint8_t* keys, const uint
         const vbf::Prefix p = host_prefix(kp, len, lp);
         uint8_t hit = 1;
         for (uint32_t i = 0; i < k; ++i) {
-            const uint32_t idx = (uint32_t)(vbf::prefix_hash(p, i) % (uint64_t)s.m);
+            const uint32_t idx = (uint32_t)(vbf::prefix_hash(p, i) % (uint64_t)m);
             if (!((w[idx >> 5] >> (idx & 31)) & 1u)) {
                 hit = 0;
                 break;
@@ -677,6 +749,21 @@ int filter_stream(int device, hipStream_t* out) {
     if ((int)g_filter_streams.size() <= device) g_filter_streams.resize(device + 1, nullptr);
     if (!g_filter_streams[device]) HIP_TRY(hipStreamCreateWithFlags(&g_filter_streams[device], hipStreamNonBlocking));
     *out = g_filter_streams[device];
+    return VBF_OK;
+}
+
+// Caller holds s.mu (drained), on s.device: the mirror holds the current bits (one D2H when
+// it is stale).
+int mirror_fill(Storage& s) {
+    int rc = storage_sync(s);
+    if (rc) return rc;
+    if (s.mirror_ok || !s.nwords) return VBF_OK;
+    if (!s.mirror) HIP_TRY(hipHostMalloc((void**)&s.mirror, s.nwords * 4, hipHostMallocDefault));
+    hipStream_t fs;
+    if ((rc = filter_stream(s.device, &fs))) return rc;
+    HIP_TRY(hipMemcpyAsync(s.mirror, s.d_words, s.nwords * 4, hipMemcpyDeviceToHost, fs));
+    HIP_TRY(hipStreamSynchronize(fs));
+    s.mirror_ok = true;
     return VBF_OK;
 }
 
@@ -843,6 +930,132 @@ int parse_index(const uint8_t* index, uint64_t len, std::vector<uint32_t>* out) 
         p += (uint64_t)L + 8;
     }
     return VBF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Host keys into a device-resident filter.  Caller holds s.mu (drained), on s.device: the keys
+// stream through the device's staging pipeline (H2D of chunk c+1 under the kernels of chunk c)
+// and the bits are merged into d_words; returns with the work finished.
+// ---------------------------------------------------------------------------------------
+int device_set_host(Storage& s, uint32_t k, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                    uint64_t n, int lp) {
+    Staging* st = staging_for(s.device);
+    std::lock_guard<std::mutex> lk2(st->mu);
+    int rc = st->init(s.device);
+    if (rc) return rc;
+    if ((rc = storage_sync(s))) return rc;  // earlier _dev work on this filter, any stream
+    s.mirror_ok = false;
+    rc = pipeline_host_keys(
+        *st, keys, offsets, stride, n, lp, false,
+        [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t hs) -> int {
+            return do_build(kb, s.m, k, s.d_words, VBF_BUILD_AUTO, true, hs);
+        },
+        [](int, uint64_t, uint64_t) { return VBF_OK; });
+    if (rc) return rc;
+    return mirror_after_write(s, st->stream[0]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Asynchronous set_host (vbf_filter_set_host_async): one worker thread per device runs the
+// queued jobs in order, each exactly as a synchronous set_host would under the filter's lock.
+// The submitting thread returns at once, so a serial caller -- the compaction loop that builds
+// one filter per merged table (compactors/sized.rs:170-200) -- keeps merging the next table
+// while the GPUs build, one filter per device with VBF_DEVICE_AUTO placement.
+// ---------------------------------------------------------------------------------------
+struct AsyncJob {
+    std::shared_ptr<Storage> s;
+    uint32_t k = 0;
+    const uint8_t* keys = nullptr;
+    const uint64_t* offsets = nullptr;
+    uint64_t stride = 0, n = 0;
+    int lp = 1;
+    std::unique_ptr<uint8_t[]> own_keys;  // the library's copy when the caller passed no release
+    std::unique_ptr<uint64_t[]> own_offs;
+    void (*release)(void*) = nullptr;
+    void* ctx = nullptr;
+};
+
+class AsyncQueue {
+  public:
+    static AsyncQueue& get(int device) {
+        static std::mutex mu;
+        static std::vector<AsyncQueue*> qs;  // never destroyed: the workers outlive static teardown
+        std::lock_guard<std::mutex> lk(mu);
+        if ((int)qs.size() <= device) qs.resize(device + 1, nullptr);
+        // a forked child inherits the queue objects but not their threads: start new ones
+        if (!qs[device] || qs[device]->pid_ != getpid()) qs[device] = new AsyncQueue();
+        return *qs[device];
+    }
+    void push(AsyncJob* j) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back(j);
+        }
+        cv_.notify_one();
+    }
+
+  private:
+    AsyncQueue() : pid_(getpid()) { std::thread([this] { loop(); }).detach(); }
+    void loop() {
+        for (;;) {
+            AsyncJob* j;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return !q_.empty(); });
+                j = q_.front();
+                q_.erase(q_.begin());
+            }
+            run(*j);
+            if (j->release) j->release(j->ctx);
+            Storage& s = *j->s;
+            {
+                std::lock_guard<std::mutex> lk(s.mu);
+                ++s.jobs_done;
+            }
+            s.jobs_cv.notify_all();
+            delete j;
+        }
+    }
+    static void run(AsyncJob& j) {
+        Storage& s = *j.s;
+        std::lock_guard<std::mutex> lk(s.mu);
+        int rc;
+        {
+            DeviceGuard g(s.device);
+            rc = g.err != hipSuccess ? fail(VBF_ENODEV, "hipSetDevice(%d): %s", s.device, hipGetErrorString(g.err))
+                                     : device_set_host(s, j.k, j.keys, j.offsets, j.stride, j.n, j.lp);
+        }
+        if (rc && s.async_rc == VBF_OK) {  // the first failure is reported by the next call that drains
+            s.async_rc = rc;
+            s.async_msg = g_err;
+        }
+    }
+    const pid_t pid_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<AsyncJob*> q_;
+};
+
+std::atomic<uint64_t> g_auto_rr{0};
+
+// xor over words of (w_i * G + (i + 1) * C), 64-bit wrapping: velarixdb_amd/filter_file.py's
+// fast_checksum, the integrity word of the persisted bit array.
+uint64_t words_checksum(const uint32_t* w, uint64_t nwords) {
+    constexpr uint64_t G = 0x9E3779B97F4A7C15ull, C = 0xC2B2AE3D27D4EB4Full;
+    CopyPool& pool = CopyPool::get();
+    const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(pool.threads(), nwords >> 20));
+    std::vector<uint64_t> part(nt, 0);
+    auto body = [&](unsigned t) {
+        const uint64_t a = nwords * t / nt, b = nwords * (t + 1) / nt;
+        uint64_t x = 0;
+        for (uint64_t i = a; i < b; ++i) x ^= (uint64_t)w[i] * G + (i + 1) * C;
+        part[t] = x;
+    };
+    if (nt == 1) body(0);
+    else pool.run(nt, body);
+    uint64_t x = 0;
+    for (uint64_t v : part) x ^= v;
+    return x;
 }
 
 }  // namespace
@@ -1143,6 +1356,11 @@ int vbf_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
 }
 
 // ---- filter handle ----
+//
+// Every entry point takes the filter's lock (Storage::mu, the reference's Mutex<BitVec>) BEFORE
+// it looks at where the bits live: vbf_filter_migrate changes device / d_words / h_words under
+// that lock and clones share the Storage, so a residency read outside it could send a call down
+// the wrong path.  Then it drains the filter's queued asynchronous sets (storage_drain).
 
 static int make_filter(int device, uint32_t m, uint32_t k, double p, vbf_filter** out) {
     if (!out) return fail(VBF_EINVAL, "out is NULL");
@@ -1154,6 +1372,9 @@ static int make_filter(int device, uint32_t m, uint32_t k, double p, vbf_filter*
         int count = 0;
         if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
             return fail(VBF_ENODEV, "no HIP device available");
+        // placement policy: filters created with VBF_DEVICE_AUTO go round-robin over the devices,
+        // so one serial caller's successive filters (one per merged table) land on different GPUs
+        if (device == VBF_DEVICE_AUTO) device = (int)(g_auto_rr.fetch_add(1) % (uint64_t)count);
         if (device < 0 || device >= count)
             return fail(VBF_ENODEV, "device %d out of range (%d devices)", device, count);
         DEVICE_SCOPE(device);
@@ -1212,8 +1433,16 @@ uint32_t vbf_filter_num_bits(const vbf_filter* f) { return f ? f->bits->m : 0; }
 uint32_t vbf_filter_num_elements(const vbf_filter* f) { return f ? f->n.load() : 0; }
 uint32_t vbf_filter_num_hash_functions(const vbf_filter* f) { return f ? f->k : 0; }
 double vbf_filter_false_positive_rate(const vbf_filter* f) { return f ? f->p : 0.0; }
-int vbf_filter_device(const vbf_filter* f) { return f ? f->bits->device : VBF_DEVICE_HOST - 1; }
-uint32_t* vbf_filter_words_dev(const vbf_filter* f) { return f ? f->bits->d_words : nullptr; }
+int vbf_filter_device(const vbf_filter* f) {
+    if (!f) return VBF_DEVICE_HOST - 1;
+    std::lock_guard<std::mutex> lk(f->bits->mu);
+    return f->bits->device;
+}
+uint32_t* vbf_filter_words_dev(const vbf_filter* f) {
+    if (!f) return nullptr;
+    std::lock_guard<std::mutex> lk(f->bits->mu);
+    return f->bits->d_words;
+}
 
 int vbf_filter_set_num_elements(vbf_filter* f, uint32_t n) {
     if (!f) return fail(VBF_EINVAL, "filter is NULL");
@@ -1231,18 +1460,21 @@ int vbf_filter_set_dev(vbf_filter* f, const uint8_t* keys, const uint64_t* offse
                        uint64_t n, int len_prefix, void* stream) {
     if (!f) return fail(VBF_EINVAL, "filter is NULL");
     Storage& s = *f->bits;
-    if (s.host()) return host_resident("vbf_filter_set_dev");
-    int rc = check_mk(s.m, f->k, n);
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
     if (rc) return rc;
+    if (s.host()) return host_resident("vbf_filter_set_dev");
+    if ((rc = check_mk(s.m, f->k, n))) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
     if (n && f->k) {
         DEVICE_SCOPE(s.device);
         const hipStream_t hs = (hipStream_t)stream;
-        std::lock_guard<std::mutex> lk(s.mu);
         if ((rc = storage_wait(s, hs))) return rc;
         vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
+        s.mirror_ok = false;
         if ((rc = do_build(kb, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, hs))) return rc;
         if ((rc = storage_mark(s, hs))) return rc;
+        if ((rc = mirror_after_write(s, hs))) return rc;
     }
     f->n.fetch_add((uint32_t)n);
     return ok();
@@ -1255,25 +1487,133 @@ int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offs
     int rc = check_mk(s.m, f->k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
-    if (n && f->k && s.host()) {
-        std::lock_guard<std::mutex> lk(s.mu);
-        host_set(s, f->k, keys, offsets, stride, n, len_prefix != 0);
-    } else if (n && f->k) {
-        DEVICE_SCOPE(s.device);
-        Staging* st = staging_for(s.device);
-        std::lock_guard<std::mutex> lk(s.mu);
-        std::lock_guard<std::mutex> lk2(st->mu);
-        if ((rc = st->init(s.device))) return rc;
-        if ((rc = storage_sync(s))) return rc;  // earlier _dev work on this filter, any stream
-        rc = pipeline_host_keys(
-            *st, keys, offsets, stride, n, len_prefix, false,
-            [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t hs) -> int {
-                return do_build(kb, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, hs);
-            },
-            [](int, uint64_t, uint64_t) { return VBF_OK; });
-        if (rc) return rc;
+    std::unique_lock<std::mutex> lk(s.mu);
+    if ((rc = storage_drain(s, lk))) return rc;
+    if (n && f->k) {
+        if (s.host()) {
+            host_set(s.h_words.data(), s.m, f->k, keys, offsets, stride, n, len_prefix != 0);
+        } else {
+            DEVICE_SCOPE(s.device);
+            if ((rc = device_set_host(s, f->k, keys, offsets, stride, n, len_prefix))) return rc;
+        }
     }
     f->n.fetch_add((uint32_t)n);
+    return ok();
+}
+
+int vbf_filter_set_host_async(vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                              uint64_t n, int len_prefix, void (*release)(void*), void* release_ctx) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    int rc = check_mk(s.m, f->k, n);
+    if (rc) return rc;
+    if ((rc = check_keys(keys, offsets, stride, n))) return rc;
+    std::unique_ptr<AsyncJob> j(new AsyncJob());
+    j->s = f->bits;
+    j->k = f->k;
+    j->stride = stride;
+    j->n = n;
+    j->lp = len_prefix;
+    j->release = release;
+    j->ctx = release_ctx;
+    if (n && f->k && !release) {
+        // no release callback: the caller may reuse its buffers on return, so the job runs from
+        // the library's own copy
+        const uint64_t base = offsets ? offsets[0] : 0;
+        const uint64_t bytes = offsets ? offsets[n] - base : n * stride;
+        j->own_keys.reset(new (std::nothrow) uint8_t[bytes ? bytes : 1]);
+        if (!j->own_keys) return fail(VBF_ENOMEM, "copying %llu key bytes", (unsigned long long)bytes);
+        if (bytes) par_memcpy(j->own_keys.get(), keys + base, bytes);
+        if (offsets) {
+            j->own_offs.reset(new (std::nothrow) uint64_t[n + 1]);
+            if (!j->own_offs) return fail(VBF_ENOMEM, "copying %llu offsets", (unsigned long long)(n + 1));
+            for (uint64_t i = 0; i <= n; ++i) j->own_offs[i] = offsets[i] - base;
+        }
+        j->keys = j->own_keys.get();
+        j->offsets = j->own_offs.get();
+    } else {
+        j->keys = keys;
+        j->offsets = offsets;
+    }
+    std::unique_lock<std::mutex> lk(s.mu);
+    if (s.host() || !n || !f->k) {  // nothing to overlap with: the CPU set runs now
+        if ((rc = storage_drain(s, lk))) return rc;
+        if (n && f->k) host_set(s.h_words.data(), s.m, f->k, j->keys, j->offsets, stride, n, len_prefix != 0);
+        lk.unlock();
+        if (release) release(release_ctx);
+    } else {
+        ++s.jobs_queued;
+        // s.device cannot change while the job is queued: migrate drains first
+        AsyncQueue::get(s.device).push(j.release());
+    }
+    f->n.fetch_add((uint32_t)n);
+    return ok();
+}
+
+int vbf_filter_sync(vbf_filter* f) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
+    if (rc) return rc;
+    if (!s.host()) {
+        DEVICE_SCOPE(s.device);
+        if ((rc = storage_sync(s))) return rc;
+    }
+    return ok();
+}
+
+int vbf_filter_busy(const vbf_filter* f) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.jobs_done != s.jobs_queued) return 1;
+    if (s.host() || !s.pending) return 0;
+    DEVICE_SCOPE(s.device);
+    const hipError_t e = hipEventQuery(s.last);
+    if (e == hipErrorNotReady) return 1;
+    if (e != hipSuccess) return fail(VBF_EHIP, "hipEventQuery: %s", hipGetErrorString(e));
+    return 0;
+}
+
+int vbf_filter_stream_wait(const vbf_filter* f, void* stream) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
+    if (rc) return rc;
+    if (s.host()) return host_resident("vbf_filter_stream_wait");
+    DEVICE_SCOPE(s.device);
+    if ((rc = storage_wait(s, (hipStream_t)stream))) return rc;
+    return ok();
+}
+
+int vbf_filter_stream_record(vbf_filter* f, void* stream) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
+    if (rc) return rc;
+    if (s.host()) return host_resident("vbf_filter_stream_record");
+    DEVICE_SCOPE(s.device);
+    if ((rc = storage_mark(s, (hipStream_t)stream))) return rc;
+    if ((rc = mirror_after_write(s, (hipStream_t)stream))) return rc;
+    return ok();
+}
+
+int vbf_filter_set_mirror(vbf_filter* f, int mode) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    if (mode < VBF_MIRROR_OFF || mode > VBF_MIRROR_EAGER) return fail(VBF_EINVAL, "unknown mirror mode %d", mode);
+    Storage& s = *f->bits;
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
+    if (rc) return rc;
+    if (!s.host()) {
+        DEVICE_SCOPE(s.device);
+        if ((rc = storage_sync(s))) return rc;  // a queued eager refresh must land before a free
+    }
+    s.mirror_mode = mode;
+    if (mode == VBF_MIRROR_OFF) s.free_mirror();
     return ok();
 }
 
@@ -1281,15 +1621,16 @@ int vbf_filter_contains_dev(const vbf_filter* f, const uint8_t* keys, const uint
                             uint64_t stride, uint64_t n, int len_prefix, uint8_t* out, void* stream) {
     if (!f) return fail(VBF_EINVAL, "filter is NULL");
     Storage& s = *f->bits;
-    if (s.host()) return host_resident("vbf_filter_contains_dev");
-    int rc = check_mk(s.m, f->k, n);
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
     if (rc) return rc;
+    if (s.host()) return host_resident("vbf_filter_contains_dev");
+    if ((rc = check_mk(s.m, f->k, n))) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
     if (n && !out) return fail(VBF_EINVAL, "out is NULL");
     if (n == 0) return ok();
     DEVICE_SCOPE(s.device);
     const hipStream_t hs = (hipStream_t)stream;
-    std::lock_guard<std::mutex> lk(s.mu);
     if ((rc = storage_wait(s, hs))) return rc;
     vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
     if ((rc = do_probe(kb, s.m, f->k, s.d_words, out, nullptr, VBF_BUILD_AUTO, hs))) return rc;
@@ -1306,14 +1647,20 @@ int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uin
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
     if (n && !out) return fail(VBF_EINVAL, "out is NULL");
     if (n == 0) return ok();
+    std::unique_lock<std::mutex> lk(s.mu);
+    if ((rc = storage_drain(s, lk))) return rc;
     if (s.host()) {
-        std::lock_guard<std::mutex> lk(s.mu);
-        host_contains(s, f->k, keys, offsets, stride, n, len_prefix != 0, out);
+        host_contains(s.h_words.data(), s.m, f->k, keys, offsets, stride, n, len_prefix != 0, out);
         return ok();
     }
     DEVICE_SCOPE(s.device);
+    if (mirror_mode(s) != VBF_MIRROR_OFF && n <= mirror_max_keys()) {
+        // the read path's single-key probes (range.rs:130,136,171) answer from the host mirror
+        if ((rc = mirror_fill(s))) return rc;
+        host_contains(s.mirror, s.m, f->k, keys, offsets, stride, n, len_prefix != 0, out);
+        return ok();
+    }
     Staging* st = staging_for(s.device);
-    std::lock_guard<std::mutex> lk(s.mu);
     std::lock_guard<std::mutex> lk2(st->mu);
     if ((rc = st->init(s.device))) return rc;
     if ((rc = storage_sync(s))) return rc;
@@ -1335,21 +1682,50 @@ int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uin
 int vbf_filter_clear(vbf_filter* f, vbf_filter** out) {
     if (!f || !out) return fail(VBF_EINVAL, "NULL argument");
     Storage& s = *f->bits;
-    if (s.host()) {
-        std::lock_guard<std::mutex> lk(s.mu);
-        std::fill(s.h_words.begin(), s.h_words.end(), 0u);
-    } else {
-        DEVICE_SCOPE(s.device);
-        std::lock_guard<std::mutex> lk(s.mu);
-        hipStream_t fs;
-        int rc = filter_stream(s.device, &fs);
+    int device;
+    {
+        std::unique_lock<std::mutex> lk(s.mu);
+        int rc = storage_drain(s, lk);
         if (rc) return rc;
-        if ((rc = storage_wait(s, fs))) return rc;  // a pending set_dev must not undo the clear
-        if (s.nwords) HIP_TRY(hipMemsetAsync(s.d_words, 0, s.nwords * 4, fs));
-        HIP_TRY(hipStreamSynchronize(fs));
-        s.pending = false;
+        if (s.host()) {
+            std::fill(s.h_words.begin(), s.h_words.end(), 0u);
+        } else {
+            DEVICE_SCOPE(s.device);
+            hipStream_t fs;
+            if ((rc = filter_stream(s.device, &fs))) return rc;
+            if ((rc = storage_wait(s, fs))) return rc;  // a pending set_dev must not undo the clear
+            if (s.nwords) HIP_TRY(hipMemsetAsync(s.d_words, 0, s.nwords * 4, fs));
+            HIP_TRY(hipStreamSynchronize(fs));
+            s.pending = false;
+            if (s.mirror) {  // the mirror stays exact: all zero too
+                std::memset(s.mirror, 0, s.nwords * 4);
+                s.mirror_ok = true;
+            }
+        }
+        device = s.device;
     }
-    return make_filter(s.device, s.m, f->k, f->p, out);
+    return make_filter(device, s.m, f->k, f->p, out);
+}
+
+// Caller holds s.mu (drained).
+static int words_to_host_locked(Storage& s, uint32_t* out) {
+    if (!s.nwords) return VBF_OK;
+    if (s.host()) {
+        std::memcpy(out, s.h_words.data(), s.nwords * 4);
+        return VBF_OK;
+    }
+    DEVICE_SCOPE(s.device);
+    int rc = storage_sync(s);  // this filter's pending work only: other filters keep running
+    if (rc) return rc;
+    if (s.mirror_ok) {  // current host copy: no PCIe transfer
+        par_memcpy(out, s.mirror, s.nwords * 4);
+        return VBF_OK;
+    }
+    Staging* st = staging_for(s.device);
+    std::lock_guard<std::mutex> lk2(st->mu);
+    rc = st->init(s.device);
+    if (!rc) rc = xfer_d2h(*st, out, s.d_words, s.nwords * 4);
+    return rc;
 }
 
 int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords) {
@@ -1357,21 +1733,33 @@ int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords
     Storage& s = *f->bits;
     if (nwords < s.nwords || (s.nwords && !out)) return fail(VBF_EINVAL, "out holds %llu < %llu words",
                                                             (unsigned long long)nwords, (unsigned long long)s.nwords);
-    if (!s.nwords) return ok();
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
+    if (!rc) rc = words_to_host_locked(s, out);
+    return rc ? rc : ok();
+}
+
+// Caller holds s.mu (drained).
+static int words_from_host_locked(Storage& s, const uint32_t* in) {
+    if (!s.nwords) return VBF_OK;
     if (s.host()) {
-        std::lock_guard<std::mutex> lk(s.mu);
-        std::memcpy(out, s.h_words.data(), s.nwords * 4);
-        return ok();
+        std::memcpy(s.h_words.data(), in, s.nwords * 4);
+        return VBF_OK;
     }
     DEVICE_SCOPE(s.device);
-    std::lock_guard<std::mutex> lk(s.mu);
-    int rc = storage_sync(s);  // this filter's pending work only: other filters keep running
+    int rc = storage_sync(s);
     if (rc) return rc;
+    s.mirror_ok = false;
     Staging* st = staging_for(s.device);
     std::lock_guard<std::mutex> lk2(st->mu);
     rc = st->init(s.device);
-    if (!rc) rc = xfer_d2h(*st, out, s.d_words, s.nwords * 4);
-    return rc ? rc : ok();
+    if (!rc) rc = xfer_h2d(*st, s.d_words, in, s.nwords * 4);
+    if (!rc && mirror_mode(s) == VBF_MIRROR_EAGER) {
+        if (!s.mirror) HIP_TRY(hipHostMalloc((void**)&s.mirror, s.nwords * 4, hipHostMallocDefault));
+        par_memcpy(s.mirror, in, s.nwords * 4);
+        s.mirror_ok = true;
+    }
+    return rc;
 }
 
 int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nwords) {
@@ -1379,20 +1767,9 @@ int vbf_filter_words_from_host(vbf_filter* f, const uint32_t* in, uint64_t nword
     Storage& s = *f->bits;
     if (nwords != s.nwords || (s.nwords && !in)) return fail(VBF_EINVAL, "expected %llu words, got %llu",
                                                             (unsigned long long)s.nwords, (unsigned long long)nwords);
-    if (!s.nwords) return ok();
-    if (s.host()) {
-        std::lock_guard<std::mutex> lk(s.mu);
-        std::memcpy(s.h_words.data(), in, s.nwords * 4);
-        return ok();
-    }
-    DEVICE_SCOPE(s.device);
-    std::lock_guard<std::mutex> lk(s.mu);
-    int rc = storage_sync(s);
-    if (rc) return rc;
-    Staging* st = staging_for(s.device);
-    std::lock_guard<std::mutex> lk2(st->mu);
-    rc = st->init(s.device);
-    if (!rc) rc = xfer_h2d(*st, s.d_words, in, s.nwords * 4);
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
+    if (!rc) rc = words_from_host_locked(s, in);
     return rc ? rc : ok();
 }
 
@@ -1402,17 +1779,19 @@ int vbf_filter_migrate(vbf_filter* f, int device) {
     if (device != VBF_DEVICE_HOST) {
         int count = 0;
         if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return fail(VBF_ENODEV, "no HIP device available");
+        if (device == VBF_DEVICE_AUTO) device = (int)(g_auto_rr.fetch_add(1) % (uint64_t)count);
         if (device < 0 || device >= count) return fail(VBF_ENODEV, "device %d out of range (%d devices)", device, count);
     }
-    std::lock_guard<std::mutex> lk(s.mu);
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
+    if (rc) return rc;
     if (device == s.device) return ok();
     std::vector<uint32_t> w;
     if (s.host()) {
         w.swap(s.h_words);
     } else {
         DEVICE_SCOPE(s.device);
-        int rc = storage_sync(s);
-        if (rc) return rc;
+        if ((rc = storage_sync(s))) return rc;
         w.resize(s.nwords);
         if (s.nwords) HIP_TRY(hipMemcpy(w.data(), s.d_words, s.nwords * 4, hipMemcpyDeviceToHost));
     }
@@ -1435,9 +1814,128 @@ int vbf_filter_migrate(vbf_filter* f, int device) {
         s.last = nullptr;
         s.pending = false;
     }
+    // a mirror of the old device copy still holds the bits; moving to the host makes it moot
+    if (device == VBF_DEVICE_HOST) s.free_mirror();
     s.d_words = nd;
     if (device == VBF_DEVICE_HOST) s.h_words.swap(w);
     s.device = device;
+    return ok();
+}
+
+// ---- persisted bit array ----
+
+static constexpr uint32_t kExtMagic = 0x57464256u;  // "VBFW"
+static constexpr uint32_t kExtVersion = 2;
+static constexpr uint64_t kExtBytes = 32;  // u32 magic | u32 version | u32 m | u32 nwords | u64 entries | u64 checksum
+
+static inline void put_u32(uint8_t* p, uint32_t v) { std::memcpy(p, &v, 4); }
+static inline void put_u64(uint8_t* p, uint64_t v) { std::memcpy(p, &v, 8); }
+static inline uint32_t get_u32(const uint8_t* p) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;
+}
+static inline uint64_t get_u64(const uint8_t* p) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    return v;
+}
+
+int vbf_filter_serialize_ext(const vbf_filter* f, const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
+                             uint64_t entries, int len_prefix, uint8_t* buf, uint64_t cap, uint64_t* len) {
+    if (!f || !len) return fail(VBF_EINVAL, "NULL argument");
+    Storage& s = *f->bits;
+    const uint32_t k = f->k, n = f->n.load();
+    const double p = f->p;
+    // recover_meta (bf.rs:144-147) recreates m from the stored n; persisted bits are useful only
+    // in that shape
+    const uint32_t m_rec = vbf_num_bits((uint64_t)n, p);
+    const uint64_t nw = ((uint64_t)m_rec + 31) / 32;
+    enum { kHeaderOnly, kOwnWords, kFromKeys } mode = kHeaderOnly;
+    if (entries != VBF_EXT_NONE && !(m_rec == 0 && k > 0 && entries > 0)) {
+        if (s.m == m_rec) mode = kOwnWords;
+        else if (keys || offsets || entries == 0) mode = kFromKeys;
+    }
+    if (mode == kFromKeys) {
+        int rc = check_keys(keys, offsets, stride, entries);
+        if (rc) return rc;
+    }
+    const uint64_t need = 16 + (mode == kHeaderOnly ? 0 : kExtBytes + nw * 4);
+    *len = need;
+    if (!buf) return ok();  // size query
+    if (cap < need) return fail(VBF_EINVAL, "buffer holds %llu < %llu bytes", (unsigned long long)cap,
+                                (unsigned long long)need);
+    vbf_meta_serialize(k, n, p, buf);
+    if (mode == kHeaderOnly) return ok();
+    uint8_t* body = buf + 16 + kExtBytes;
+    const bool aligned = ((uintptr_t)body & 3) == 0;
+    std::vector<uint32_t> tmp;
+    uint32_t* w = reinterpret_cast<uint32_t*>(body);
+    if (!aligned) {
+        tmp.resize(nw);
+        w = tmp.data();
+    }
+    int rc = VBF_OK;
+    if (mode == kOwnWords) {
+        std::unique_lock<std::mutex> lk(s.mu);
+        rc = storage_drain(s, lk);
+        if (!rc) rc = words_to_host_locked(s, w);
+    } else {
+        std::memset(w, 0, nw * 4);
+        if (entries && k) {
+            int device;
+            {
+                std::lock_guard<std::mutex> lk(s.mu);
+                device = s.device;
+            }
+            if (device == VBF_DEVICE_HOST) host_set(w, m_rec, k, keys, offsets, stride, entries, len_prefix != 0);
+            else rc = vbf_build_host(keys, offsets, stride, entries, len_prefix, m_rec, k, w, nw, device);
+        }
+    }
+    if (rc) return rc;
+    if (!aligned) std::memcpy(body, tmp.data(), nw * 4);
+    uint8_t* e = buf + 16;
+    put_u32(e, kExtMagic);
+    put_u32(e + 4, kExtVersion);
+    put_u32(e + 8, m_rec);
+    put_u32(e + 12, (uint32_t)nw);
+    put_u64(e + 16, entries);
+    put_u64(e + 24, words_checksum(w, nw));
+    return ok();
+}
+
+int vbf_filter_recover_ext(const uint8_t* bytes, uint64_t len, int device, vbf_filter** out, int* restored) {
+    if (!bytes || !out) return fail(VBF_EINVAL, "NULL argument");
+    if (restored) *restored = 0;
+    vbf_filter* f = nullptr;
+    int rc = vbf_filter_recover(bytes, (size_t)len, device, &f);
+    if (rc) return rc;
+    const uint32_t m = f->bits->m;
+    const uint64_t nw = ((uint64_t)m + 31) / 32;
+    if (len >= 16 + kExtBytes) {
+        const uint8_t* e = bytes + 16;
+        const uint8_t* body = e + kExtBytes;
+        if (get_u32(e) == kExtMagic && get_u32(e + 4) == kExtVersion && get_u32(e + 8) == m &&
+            get_u32(e + 12) == nw && len - 16 - kExtBytes == nw * 4) {
+            std::vector<uint32_t> tmp;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(body);
+            if ((uintptr_t)body & 3) {
+                tmp.resize(nw);
+                std::memcpy(tmp.data(), body, nw * 4);
+                w = tmp.data();
+            }
+            if (words_checksum(w, nw) == get_u64(e + 24)) {
+                if ((rc = vbf_filter_words_from_host(f, w, nw))) {
+                    vbf_filter_free(f);
+                    return rc;
+                }
+                // recover_meta + build_filter_from_entries (range.rs:121-124): stored n + entries
+                f->n.store((uint32_t)(f->n.load() + get_u64(e + 16)));
+                if (restored) *restored = 1;
+            }
+        }
+    }
+    *out = f;
     return ok();
 }
 
@@ -1525,13 +2023,9 @@ int vbf_sst_decode_host(const uint8_t* data, uint64_t len, const uint8_t* index,
 
 // range.rs:117-128 (load_entries_from_file + build_filter_from_entries) on the device: decode
 // data.db into packed keys/offsets and OR their bits into the filter; no_of_elements += n.
-int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t len, const uint32_t* blocks,
-                                    uint64_t nblocks, uint64_t* n_out, void* stream) {
-    if (!f) return fail(VBF_EINVAL, "filter is NULL");
-    Storage& s = *f->bits;
-    if (s.host()) return host_resident("vbf_filter_rebuild_from_sst_dev");
-    DEVICE_SCOPE(s.device);
-    hipStream_t st = (hipStream_t)stream;
+// Caller holds s.mu (drained), on s.device; the filter is device-resident.
+static int rebuild_locked(vbf_filter* f, Storage& s, const uint8_t* data, uint64_t len, const uint32_t* blocks,
+                          uint64_t nblocks, uint64_t* n_out, hipStream_t st) {
     uint64_t n = 0;
     vbf::SstArgs a;
     uint32_t ulen = 0xFFFFFFFFu;
@@ -1549,13 +2043,27 @@ int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t
         // the build reads with its aligned fast path instead of through offsets
         const bool uniform = ulen != 0xFFFFFFFFu && ulen > 0;
         if ((rc = sst_emit_pass(a, d_keys, uniform ? nullptr : d_off, nullptr, nullptr, nullptr, st))) return rc;
-        std::lock_guard<std::mutex> lk(s.mu);
         if ((rc = storage_wait(s, st))) return rc;
         vbf::KeyBatch kb2 = uniform ? batch(d_keys, nullptr, 0, ulen, n, 1) : batch(d_keys, d_off, 0, 0, n, 1);
+        s.mirror_ok = false;
         if ((rc = do_build(kb2, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, st))) return rc;
         if ((rc = storage_mark(s, st))) return rc;
+        if ((rc = mirror_after_write(s, st))) return rc;
     }
     f->n.fetch_add((uint32_t)n);
+    return VBF_OK;
+}
+
+int vbf_filter_rebuild_from_sst_dev(vbf_filter* f, const uint8_t* data, uint64_t len, const uint32_t* blocks,
+                                    uint64_t nblocks, uint64_t* n_out, void* stream) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    Storage& s = *f->bits;
+    std::unique_lock<std::mutex> lk(s.mu);
+    int rc = storage_drain(s, lk);
+    if (rc) return rc;
+    if (s.host()) return host_resident("vbf_filter_rebuild_from_sst_dev");
+    DEVICE_SCOPE(s.device);
+    if ((rc = rebuild_locked(f, s, data, len, blocks, nblocks, n_out, (hipStream_t)stream))) return rc;
     return ok();
 }
 
@@ -1563,10 +2071,12 @@ int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_
                                      uint64_t index_len, uint64_t* n_out) {
     if (!f || (len && !data) || (index_len && !index)) return fail(VBF_EINVAL, "NULL argument");
     Storage& s = *f->bits;
-    if (s.host()) return host_resident("vbf_filter_rebuild_from_sst_host");
     std::vector<uint32_t> blk;
     int rc = parse_index(index, index_len, &blk);
     if (rc) return rc;
+    std::unique_lock<std::mutex> lk(s.mu);
+    if ((rc = storage_drain(s, lk))) return rc;
+    if (s.host()) return host_resident("vbf_filter_rebuild_from_sst_host");
     DEVICE_SCOPE(s.device);
     hipStream_t st;
     if ((rc = filter_stream(s.device, &st))) return rc;
@@ -1577,7 +2087,7 @@ int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_
     uint32_t* d_blk = reinterpret_cast<uint32_t*>(d_data + o_blk);
     if (len) HIP_TRY(hipMemcpyAsync(d_data, data, len, hipMemcpyHostToDevice, st));
     if (blk.size()) HIP_TRY(hipMemcpyAsync(d_blk, blk.data(), blk.size() * 4, hipMemcpyHostToDevice, st));
-    if ((rc = vbf_filter_rebuild_from_sst_dev(f, d_data, len, d_blk, blk.size(), n_out, st))) return rc;
+    if ((rc = rebuild_locked(f, s, d_data, len, d_blk, blk.size(), n_out, st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     return ok();
 }
@@ -1588,17 +2098,61 @@ int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_
 
 namespace {
 // Locks every distinct storage of `filters` in address order (clones share one), so two
-// concurrent multi-probes over overlapping sets cannot deadlock.
+// concurrent multi-probes over overlapping sets cannot deadlock; then drains each filter's
+// queued asynchronous sets (a worker needs only its own filter's lock, which the wait releases).
 struct MultiLock {
     std::vector<std::unique_lock<std::mutex>> locks;
+    std::vector<Storage*> v;
     explicit MultiLock(const vbf_filter* const* filters, uint32_t nsst) {
-        std::vector<Storage*> v;
-        for (uint32_t s = 0; s < nsst; ++s) v.push_back(filters[s]->bits.get());
+        for (uint32_t s = 0; s < nsst; ++s)
+            if (filters[s]) v.push_back(filters[s]->bits.get());
         std::sort(v.begin(), v.end());
         v.erase(std::unique(v.begin(), v.end()), v.end());
         for (Storage* st : v) locks.emplace_back(st->mu);
     }
+    int drain() {
+        for (size_t i = 0; i < v.size(); ++i)
+            if (int rc = storage_drain(*v[i], locks[i])) return rc;
+        return VBF_OK;
+    }
 };
+
+// Rust's Ord for [u8]: bytewise, then shorter first.
+int cmp_host(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
+    const int c = std::memcmp(a, b, std::min(la, lb));
+    if (c) return c < 0 ? -1 : 1;
+    return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+// The read path's small batches (one get: one key against every in-range SST,
+// range.rs:101-136) answered on the CPU from the filters' host mirrors; the same answers as the
+// k_multi_probe kernel.  Caller holds every filter's lock (drained), on their device.
+int multi_probe_mirror(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
+                       uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
+                       const uint64_t* bounds_off, uint8_t* out) {
+    for (uint32_t i = 0; i < nsst; ++i)
+        if (int rc = mirror_fill(*filters[i]->bits)) return rc;
+    for (uint64_t j = 0; j < n; ++j) {
+        const uint8_t* kp;
+        uint64_t kl;
+        host_key(keys, offsets, stride, j, &kp, &kl);
+        for (uint32_t i = 0; i < nsst; ++i) {
+            const Storage& st = *filters[i]->bits;
+            const uint32_t k = filters[i]->k;
+            bool hit = true;
+            if (bounds_off)  // range.rs:118
+                hit = cmp_host(kp, kl, bounds + bounds_off[2 * i], bounds_off[2 * i + 1] - bounds_off[2 * i]) >= 0 &&
+                      cmp_host(kp, kl, bounds + bounds_off[2 * i + 1], bounds_off[2 * i + 2] - bounds_off[2 * i + 1]) <= 0;
+            if (hit && k > 0 && st.m == 0)
+                return fail(VBF_EDIVZERO, "a key inside an SST's range reaches its filter with m == 0 < k "
+                                          "(bf.rs:100 divides by zero)");
+            uint8_t h = hit ? 1 : 0;
+            if (hit && k > 0) host_contains(st.mirror, st.m, k, kp, nullptr, kl, 1, len_prefix != 0, &h);
+            out[j * nsst + i] = h;
+        }
+    }
+    return VBF_OK;
+}
 
 int multi_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
                 uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds, const uint64_t* bounds_off,
@@ -1730,9 +2284,10 @@ int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t s
     int rc = check_keys(keys, offsets, stride, n);
     if (rc) return rc;
     if (nsst && filters && filters[0]) {
+        MultiLock lk(filters, nsst);
+        if ((rc = lk.drain())) return rc;
         if (filters[0]->bits->host()) return host_resident("vbf_multi_probe_dev");
         DEVICE_SCOPE(filters[0]->bits->device);
-        MultiLock lk(filters, nsst);
         if ((rc = multi_probe(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out,
                               (hipStream_t)stream)))
             return rc;
@@ -1756,10 +2311,32 @@ int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t 
     }
     if (!filters || !filters[0]) return fail(VBF_EINVAL, "filters is NULL");
     if (!out) return fail(VBF_EINVAL, "out is NULL");
+    MultiLock lk(filters, nsst);
+    if ((rc = lk.drain())) return rc;
     if (filters[0]->bits->host()) return host_resident("vbf_multi_probe_host");
-    DEVICE_SCOPE(filters[0]->bits->device);
+    const int device = filters[0]->bits->device;
+    DEVICE_SCOPE(device);
+    bool mirrored = n <= mirror_max_keys();
+    for (uint32_t i = 0; i < nsst && mirrored; ++i) {
+        if (!filters[i]) return fail(VBF_EINVAL, "filters[%u] is NULL", i);
+        const Storage& st = *filters[i]->bits;
+        if (st.host()) return host_resident("vbf_multi_probe_host");
+        if (st.device != device)
+            return fail(VBF_EINVAL, "filters[%u] lives on device %d, filters[0] on %d", i, st.device, device);
+        if (mirror_mode(st) == VBF_MIRROR_OFF) mirrored = false;
+    }
+    if (mirrored) {
+        if (bounds_off) {
+            for (uint32_t i = 0; i < 2 * nsst; ++i)
+                if (bounds_off[i + 1] < bounds_off[i]) return fail(VBF_EINVAL, "bounds_off not nondecreasing at %u", i);
+            if (bounds_off[2 * nsst] && !bounds) return fail(VBF_EINVAL, "bounds is NULL");
+        }
+        if ((rc = multi_probe_mirror(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out)))
+            return rc;
+        return ok();
+    }
     hipStream_t s;
-    if ((rc = filter_stream(filters[0]->bits->device, &s))) return rc;
+    if ((rc = filter_stream(device, &s))) return rc;
     const uint64_t kbytes = offsets ? offsets[n] - offsets[0] : n * stride;
     const uint64_t o_off = align256(kbytes), o_out = o_off + align256(offsets ? (n + 1) * 8 : 0);
     void* ws = nullptr;
@@ -1776,11 +2353,8 @@ int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t 
         HIP_TRY(hipMemcpyAsync(d_off, o.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
-    {
-        MultiLock lk(filters, nsst);
-        if ((rc = multi_probe(d_keys, d_off, stride, n, len_prefix, nsst, filters, bounds, bounds_off, d_out, s)))
-            return rc;
-    }
+    if ((rc = multi_probe(d_keys, d_off, stride, n, len_prefix, nsst, filters, bounds, bounds_off, d_out, s)))
+        return rc;
     HIP_TRY(hipMemcpyAsync(out, d_out, n * nsst, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return ok();

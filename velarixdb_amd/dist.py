@@ -49,16 +49,28 @@ def padded_words(nwords, world, device):
 
 def or_allreduce_(buf, chunk, group=None, or_into=or_words_dev):
     """In place: buf (padded_words layout) becomes the OR of every rank's buf.  The local OR is
-    the HIP kernel; the CPU (gloo) tests of the exchange pattern pass their own `or_into`."""
+    the HIP kernel; the CPU (gloo) tests of the exchange pattern pass their own `or_into`.
+
+    Device words under a gloo group (the one-GPU rehearsal of the N > 1 path, where RCCL refuses
+    two ranks on one card) move through host tensors for gloo's all_to_all / all_gather, while
+    the fold stays on the GPU: the same HIP OR kernel the RCCL path runs."""
     if not dist.is_initialized():
         return buf
     world = dist.get_world_size(group)
     if world == 1:
         return buf
-    recv = torch.empty_like(buf)
-    dist.all_to_all_single(recv, buf, group=group)
-    acc = recv[:chunk].clone()
+    staged = buf.device.type == "cuda" and dist.get_backend(group) == "gloo"
+    src = buf.cpu() if staged else buf
+    recv = torch.empty_like(src)
+    dist.all_to_all_single(recv, src, group=group)
+    parts = recv.to(buf.device) if staged else recv
+    acc = parts[:chunk].clone()
     for r in range(1, world):
-        or_into(acc, recv[r * chunk:(r + 1) * chunk])
-    dist.all_gather_into_tensor(buf, acc, group=group)
+        or_into(acc, parts[r * chunk:(r + 1) * chunk])
+    if staged:
+        full = torch.empty_like(src)
+        dist.all_gather_into_tensor(full, acc.cpu(), group=group)
+        buf.copy_(full)
+    else:
+        dist.all_gather_into_tensor(buf, acc, group=group)
     return buf

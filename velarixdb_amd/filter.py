@@ -19,26 +19,36 @@ Batch forms (set_many / contains_many and the *_dev variants taking device point
 accelerated entry points the compaction build (compactors/sized.rs:192-193), the lazy
 recovery rebuild (key_range/range.rs:117-128) and bulk probes use.
 
-Residency: `device` is a GPU index (bits in HBM, kernels) or HOST (bits in host memory, set /
-contains on the CPU inside libvbf with the kernels' SipHash rounds) -- the memtable's filter,
-one contains + set per put (memtable/mem.rs:207-221).  migrate() moves the bits in place.
+Residency: `device` is a GPU index (bits in HBM, kernels), "auto" (the library picks a GPU,
+round-robin) or HOST (bits in host memory, set / contains on the CPU inside libvbf with the
+kernels' SipHash rounds) -- the memtable's filter, one contains + set per put
+(memtable/mem.rs:207-221).  migrate() moves the bits in place.  A device-resident filter keeps a
+host mirror of its bits, so single-key contains (the read path, range.rs:130,136,171) answer on
+the CPU; set_mirror() tunes it.
 """
 import ctypes
 import os
 
 import numpy as np
 
-from . import _lib, filter_file
-from ._lib import VBF_DEVICE_HOST, VBF_EDIVZERO, VBF_EINVAL, VbfError, call, lib
+from . import _lib
+from ._lib import (VBF_DEVICE_AUTO, VBF_DEVICE_HOST, VBF_EDIVZERO, VBF_EINVAL, VBF_EXT_NONE, VBF_MIRROR_EAGER,
+                   VBF_MIRROR_LAZY, VBF_MIRROR_OFF, VbfError, call, lib)
 from .keys import HostBatch, encode, pack
 
 FILTER_FILE_NAME = "filter"  # consts/mod.rs:27
 DEFAULT_FALSE_POSITIVE_RATE = 1e-4  # consts/mod.rs:17
 HOST = VBF_DEVICE_HOST  # device= for a host-resident (memtable) filter
+AUTO = VBF_DEVICE_AUTO  # device= for library placement (round-robin over the GPUs)
+MIRROR_MODES = {"off": VBF_MIRROR_OFF, "lazy": VBF_MIRROR_LAZY, "eager": VBF_MIRROR_EAGER}
 
 
 def _dev(device):
-    return VBF_DEVICE_HOST if (device == "host" or device == HOST) else int(device)
+    if device == "host":
+        return VBF_DEVICE_HOST
+    if device == "auto":
+        return VBF_DEVICE_AUTO
+    return int(device)
 
 
 def num_bits(n, p):
@@ -68,7 +78,6 @@ class BloomFilter:
         self.sst_dir = None
         self.file_path = None
         self.bits_restored = False
-        self.restored_entries = None
         if _handle is not None:
             self._h = _handle
             return
@@ -190,6 +199,30 @@ class BloomFilter:
     def set_many(self, keys):
         self.set_batch(keys if isinstance(keys, HostBatch) else pack(keys))
 
+    def set_many_async(self, keys):
+        """set_many that returns before the GPU work is done (vbf_filter_set_host_async; the
+        library copies the keys first).  Later calls on the filter wait for it; sync() waits."""
+        b = keys if isinstance(keys, HostBatch) else pack(keys)
+        d, o = b.ptrs()
+        try:
+            call("vbf_filter_set_host_async", self._h, d, o, b.stride, b.n, b.len_prefix, None, None)
+        except VbfError as e:
+            _raise("set", e)
+
+    def sync(self):
+        """Wait for the filter's queued and in-flight work (raises a queued set's failure)."""
+        call("vbf_filter_sync", self._h)
+
+    def busy(self):
+        rc = lib.vbf_filter_busy(self._h)
+        if rc < 0:
+            _lib.check("vbf_filter_busy", rc)
+        return bool(rc)
+
+    def set_mirror(self, mode):
+        """Host-mirror mode of a device-resident filter: "off", "lazy" (default) or "eager"."""
+        call("vbf_filter_set_mirror", self._h, MIRROR_MODES[mode] if isinstance(mode, str) else int(mode))
+
     def contains_many(self, keys):
         return self.contains_batch(keys if isinstance(keys, HostBatch) else pack(keys))
 
@@ -241,19 +274,17 @@ class BloomFilter:
 
     def recover_from_sst_dir(self, sst_dir):
         """The lazy recovery of range.rs:117-128 for one SST directory: recover_meta() from its
-        filter.db, then -- unless persisted bits were restored (filter_file.py) -- rebuild from
-        data.db + index.db.  Returns True when the bits came from filter.db.  Either way the
-        filter ends as the reference's recover_meta + build_filter_from_entries leaves it: the
-        same bits and no_of_elements = stored n + the SST's entries."""
+        filter.db, then -- unless persisted bits were restored (vbf_filter_recover_ext) --
+        rebuild from data.db + index.db.  Returns True when the bits came from filter.db.  Either
+        way the filter ends as the reference's recover_meta + build_filter_from_entries leaves
+        it: the same bits and no_of_elements = stored n + the SST's entries."""
         from . import sst
         self.file_path = os.path.join(os.fspath(sst_dir), FILTER_FILE_NAME + ".db")
-        if self.recover_meta():
-            self.sst_dir = os.fspath(sst_dir)
-            self.set_num_elements(self.no_of_elements + self.restored_entries)
-            return True
+        restored = self.recover_meta()
         self.sst_dir = os.fspath(sst_dir)
-        self.rebuild_from_sst(*sst.read_sst_files(sst_dir))
-        return False
+        if not restored:
+            self.rebuild_from_sst(*sst.read_sst_files(sst_dir))
+        return restored
 
     # -- bits ----------------------------------------------------------------------------
     def words(self, out=None):
@@ -287,18 +318,38 @@ class BloomFilter:
         call("vbf_filter_serialize", self._h, buf)
         return bytes(buf)
 
-    def write(self, dir_path, persist_bits=True, sst_entries=None):
+    def serialize_ext(self, sst_entries=None, sst_keys=None):
+        """filter.db bytes (vbf_filter_serialize_ext): the reference's 16 bytes (bf.rs:158-172),
+        then -- when `sst_entries` (the SST's data.db entry count) is given -- the bit array a
+        restart's rebuild would produce (range.rs:117-128): this filter's own words when its m is
+        the recovery m (a compaction-built filter), otherwise built from `sst_keys` (the SST's
+        keys; a memtable-born filter).  Without them only the 16 bytes (the reference's file)."""
+        entries = VBF_EXT_NONE if sst_entries is None else int(sst_entries)
+        d = o = None
+        stride, lp = 0, 1
+        b = None
+        if sst_keys is not None and sst_entries is not None:
+            b = sst_keys if isinstance(sst_keys, HostBatch) else pack(sst_keys)
+            if b.n != entries:
+                raise ValueError("sst_keys holds %d keys, sst_entries says %d" % (b.n, entries))
+            d, o = b.ptrs()
+            stride, lp = b.stride, b.len_prefix
+        need = ctypes.c_uint64()
+        call("vbf_filter_serialize_ext", self._h, d, o, stride, entries, lp, None, 0, ctypes.byref(need))
+        buf = np.zeros(need.value, dtype=np.uint8)
+        call("vbf_filter_serialize_ext", self._h, d, o, stride, entries, lp, buf.ctypes.data, buf.size,
+             ctypes.byref(need))
+        return buf[:need.value].tobytes()
+
+    def write(self, dir_path, persist_bits=True, sst_entries=None, sst_keys=None):
         """bf.rs:114-123: write `filter.db` and remember its path.
 
-        The first 16 bytes are exactly the reference's.  With persist_bits the bit array follows
-        (filter_file.py): invisible to the reference's reader, used by recover_meta() here.
-        `sst_entries` is the SST's entry count (default no_of_elements, exact for a filter built
-        from its table's entries as compaction builds it)."""
+        The first 16 bytes are exactly the reference's.  With persist_bits and `sst_entries` the
+        bit array follows (serialize_ext): invisible to the reference's reader, restored by
+        recover_meta() here instead of a rebuild.  The writer that knows the SST passes its entry
+        count (and, for a memtable-born filter, its keys); nothing is persisted otherwise."""
         path = os.path.join(os.fspath(dir_path), FILTER_FILE_NAME + ".db")
-        m = self.num_bits()
-        words = self.words() if (persist_bits and m) else None
-        raw = filter_file.encode(self.no_of_hash_func, self.no_of_elements, self.false_positive_rate,
-                                 m, words, sst_entries)
+        raw = self.serialize_ext(sst_entries if persist_bits else None, sst_keys)
         assert raw[:16] == self.serialize()
         with open(path, "wb") as f:
             f.write(raw)
@@ -307,9 +358,10 @@ class BloomFilter:
     def recover_meta(self, load_bits=True):
         """bf.rs:135-150: k and n from filter.db, m recomputed from n, zeroed bits.
 
-        Returns True when persisted bits were loaded (their m equals the recomputed m, so they
-        equal what the reference's rebuild from data.db produces and the rebuild can be
-        skipped); False when the caller must rebuild, as the reference always does."""
+        Returns True when persisted bits were loaded (vbf_filter_recover_ext: their m equals the
+        recomputed m and the checksum holds, so they equal what the reference's rebuild from
+        data.db produces, and no_of_elements is n + entries as after that rebuild): the caller
+        skips the rebuild.  False when the caller must rebuild, as the reference always does."""
         if self.file_path is None:
             raise FileNotFoundError("File path for filter not provided (err/mod.rs:19-20)")
         try:
@@ -317,17 +369,19 @@ class BloomFilter:
                 raw = f.read()
         except OSError:
             raise FileNotFoundError("Error opening filter file %s" % self.file_path) from None
-        k, n, p, m_saved, words, entries = filter_file.decode(raw)
-        meta = (ctypes.c_uint8 * 16).from_buffer_copy(raw[:16])
+        if len(raw) < 16:
+            raise EOFError("unexpected EOF: filter metadata is %d < 16 bytes" % len(raw))
+        if not load_bits:
+            raw = raw[:16]
+        src = np.frombuffer(raw, dtype=np.uint8)
         h = ctypes.c_void_p()
-        call("vbf_filter_recover", meta, 16, self.device, ctypes.byref(h))
+        restored = ctypes.c_int(0)
+        call("vbf_filter_recover_ext", src.ctypes.data, src.size, self.device, ctypes.byref(h),
+             ctypes.byref(restored))
         old = self._h
         self._h = h
         lib.vbf_filter_free(old)
-        self.bits_restored = bool(load_bits and words is not None and m_saved == self.num_bits())
-        self.restored_entries = entries if self.bits_restored else None
-        if self.bits_restored:
-            self.load_words(words)
+        self.bits_restored = bool(restored.value)
         return self.bits_restored
 
     def __repr__(self):
