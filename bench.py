@@ -115,8 +115,6 @@ from velarixdb_amd._lib import call  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32 lane-ops/s)
-# VALU lane-instructions per key of the build, from rocprofv3 SQ_INSTS_VALU (profiles/r01)
-VALU_PER_KEY_CFG2 = 1611.0
 
 
 # rocprofv3 names of the build's kernels, and the summary of the same command, per (key bytes, k)
@@ -128,15 +126,19 @@ ROCPROF = {
 }
 
 
-def pmc_sq(name):
-    """VALU issue busy and wait fractions of k_tile_pack from one rocprofv3 SQ pass
-    (tools/pmc_sq.py); the newest round's."""
-    for rnd in ("r02",):
+SQ_FILES = {10: "sq_tile_pack.json", 19: "sq_tile_pack_k19.json"}
+
+
+def pmc_sq(name, keys):
+    """VALU issue busy, wait fractions and VALU lane-instructions per key of k_tile_pack from one
+    rocprofv3 SQ pass (tools/pmc_sq.py) over a build of `keys` keys; the newest round's."""
+    for rnd in ("r03", "r02"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             with open(path) as f:
                 d = json.load(f)
             return {"valu_issue_busy": d["valu_issue_busy"], "wave_wait_any_frac": d["wave_wait_any_frac"],
+                    "valu_lane_instr_per_key": d["counters_per_dispatch"]["SQ_INSTS_VALU"] * 64 / keys,
                     "source": "profiles/%s/%s" % (rnd, name)}
         except (OSError, ValueError, KeyError):
             continue
@@ -146,7 +148,7 @@ def pmc_sq(name):
 def pmc_traffic(name, kernel=None):
     """HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes (the newest round's
     measurement): (one launch of `kernel` -- read + write --, one whole build, source file)."""
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             with open(path) as f:
@@ -415,8 +417,9 @@ def bench_fixed(ctx, args):
     # the contract's traffic: HBM bytes of one launch of the dominant kernel (like `achieved`);
     # the whole build's bytes beside it
     dom_kernel = (ROCPROF.get((L, k), ({}, None))[0] or {}).get(dom)
-    traffic, traffic_build, traffic_src = (pmc_traffic("traffic_config2.json", dom_kernel)
-                                           if (n, L, k) == (100_000_000, 16, 10) and args.strategy != 1
+    traffic_file = {10: "traffic_config2.json", 19: "traffic_config2_k19.json"}.get(k)
+    traffic, traffic_build, traffic_src = (pmc_traffic(traffic_file, dom_kernel)
+                                           if (n, L) == (100_000_000, 16) and traffic_file and args.strategy != 1
                                            else (None, None, None))
     per_rank = ctx.gather({"rank": ctx.rank, "device": ctx.local, "keys": n, "seed": seed,
                            "keys_per_s": n * args.steps / rank_wall, "ms_per_step": rank_wall / args.steps * 1e3,
@@ -426,6 +429,8 @@ def bench_fixed(ctx, args):
                 if args.config == 4 else
                 "config2: %dM x %dB keys%s, %d bits/key (m=%d, k=%d)" % (
                     n // 10**6, L, "" if ctx.world == 1 else " per GPU", args.bits_per_key, m, k))
+    # the SQ pass of the same build shape (config 2's 100M x 16 B keys at k = 10 or 19)
+    sq = pmc_sq(SQ_FILES[k], 100_000_000) if (n, L) == (100_000_000, 16) and k in SQ_FILES else None
     res = {
         "metric": "Bloom build keys/s (device-resident keys, bit-exact SipHash-1-3 filter)",
         "value": value, "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps,
@@ -441,9 +446,9 @@ def bench_fixed(ctx, args):
                      "build_ms": kavg * 1e3, "build_frac": n * bytes_per_key / kavg / 1e9 / HBM_PEAK_GBS,
                      "rocprof_kernels": ROCPROF.get((L, k), (None, None))[0],
                      "rocprof_summary": ROCPROF.get((L, k), (None, None))[1],
-                     "valu_frac_est": (n * VALU_PER_KEY_CFG2 / dom_s / VALU_PEAK_LANE_OPS
-                                       if (L, k) == (16, 10) else None),
-                     "sq_counters": pmc_sq("sq_tile_pack.json") if (n, L, k) == (100_000_000, 16, 10) else None,
+                     "valu_frac_est": (n * sq["valu_lane_instr_per_key"] / dom_s / VALU_PEAK_LANE_OPS
+                                       if sq else None),
+                     "sq_counters": sq,
                      "algorithmic_bytes_per_key": bytes_per_key,
                      "siprounds_per_key": (L + 8) // 8 + 5 * k,
                      "phases": ph},

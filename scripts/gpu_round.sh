@@ -60,6 +60,14 @@ for s in $STEPS; do
     pmc3) (cd /tmp && run pmc3 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc3" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     pmcsq) (cd /tmp && run pmcsq 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcsq" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     pmc4) (cd /tmp && run pmc4 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc4" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    sstt)   run pytest_sst 300 python -u -m pytest tests/test_gpu_sst.py -x -v -m gpu --timeout 120 --timeout-method thread ;;
+    k3sweep) run k3_sweep 900 bash tools/k3_sweep.sh ;;
+    pmcsq19) (cd /tmp && run pmcsq19 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcsq19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    pmc2_19) (cd /tmp && run pmc2_19 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc2_19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    pmc3_19) (cd /tmp && run pmc3_19 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc3_19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    pmctcc) (cd /tmp && run pmctcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum --output-format csv -d "$OUT/pmctcc" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    pmctcc19) (cd /tmp && run pmctcc19 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum --output-format csv -d "$OUT/pmctcc19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    pmctcp) (cd /tmp && run pmctcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum --output-format csv -d "$OUT/pmctcp" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     prof)   (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 40 --warmup 5 --no-cpu-baseline) || exit $? ;;
   esac
 done

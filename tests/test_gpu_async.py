@@ -264,3 +264,26 @@ def test_migrate_races_set_and_contains_on_a_clone(vbf, ora):
         th.join()
     assert not errs, errs
     assert np.array_equal(bf.words(), ora.build_words(pack(keys), bf.num_bits(), bf.no_of_hash_func))
+
+
+def test_migrate_of_a_pristine_filter_moves_no_bits(vbf, ora):
+    """A filter no key was set in since new / clear (BitVec::from_elem, bf.rs:71) migrates by
+    allocating zeroed words on the target; one with bits copies them.  The Rust patch moves a
+    fresh compaction filter to its GPU (VBF_DEVICE_AUTO) before the batch build."""
+    from velarixdb_amd import HOST
+    from velarixdb_amd.keys import pack
+    keys = [b"pm%06d" % i for i in range(50000)]
+    f = vbf.BloomFilter(0.01, 1_000_000, device=HOST)
+    f.migrate("auto")
+    assert not f.host_resident and not f.words().any()
+    f.set_many(keys)
+    f.migrate(HOST)
+    want = ora.build_words(pack(keys), f.num_bits(), f.no_of_hash_func)
+    assert f.host_resident and np.array_equal(f.words(), want)
+    f.migrate(0)
+    assert np.array_equal(f.words(), want)
+    f.clear()
+    f.migrate(HOST)
+    assert not f.words().any()
+    f.migrate(0)
+    assert not f.words().any() and not f.contains(keys[0])

@@ -581,6 +581,9 @@ struct Storage {
     // filled; filled lazily by the first small contains (one D2H), or queued right after every
     // device write in VBF_MIRROR_EAGER mode.
     int mirror_mode = -1;  // -1: the process default (VBF_MIRROR, default lazy)
+    // No bit was ever set since the array was created or cleared (BitVec::from_elem(m, false),
+    // bf.rs:71): a migrate allocates zeroed words on the target instead of copying them.
+    bool pristine = true;
     uint32_t* mirror = nullptr;
     bool mirror_ok = false;
     bool host() const { return device == VBF_DEVICE_HOST; }
@@ -945,6 +948,7 @@ int device_set_host(Storage& s, uint32_t k, const uint8_t* keys, const uint64_t*
     if (rc) return rc;
     if ((rc = storage_sync(s))) return rc;  // earlier _dev work on this filter, any stream
     s.mirror_ok = false;
+    s.pristine = false;
     rc = pipeline_host_keys(
         *st, keys, offsets, stride, n, lp, false,
         [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t hs) -> int {
@@ -1472,6 +1476,7 @@ int vbf_filter_set_dev(vbf_filter* f, const uint8_t* keys, const uint64_t* offse
         if ((rc = storage_wait(s, hs))) return rc;
         vbf::KeyBatch kb = batch(keys, offsets, 0, stride, n, len_prefix);
         s.mirror_ok = false;
+        s.pristine = false;
         if ((rc = do_build(kb, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, hs))) return rc;
         if ((rc = storage_mark(s, hs))) return rc;
         if ((rc = mirror_after_write(s, hs))) return rc;
@@ -1491,6 +1496,7 @@ int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offs
     if ((rc = storage_drain(s, lk))) return rc;
     if (n && f->k) {
         if (s.host()) {
+            s.pristine = false;
             host_set(s.h_words.data(), s.m, f->k, keys, offsets, stride, n, len_prefix != 0);
         } else {
             DEVICE_SCOPE(s.device);
@@ -1538,11 +1544,15 @@ int vbf_filter_set_host_async(vbf_filter* f, const uint8_t* keys, const uint64_t
     std::unique_lock<std::mutex> lk(s.mu);
     if (s.host() || !n || !f->k) {  // nothing to overlap with: the CPU set runs now
         if ((rc = storage_drain(s, lk))) return rc;
-        if (n && f->k) host_set(s.h_words.data(), s.m, f->k, j->keys, j->offsets, stride, n, len_prefix != 0);
+        if (n && f->k) {
+            s.pristine = false;
+            host_set(s.h_words.data(), s.m, f->k, j->keys, j->offsets, stride, n, len_prefix != 0);
+        }
         lk.unlock();
         if (release) release(release_ctx);
     } else {
         ++s.jobs_queued;
+        s.pristine = false;
         // s.device cannot change while the job is queued: migrate drains first
         AsyncQueue::get(s.device).push(j.release());
     }
@@ -1596,6 +1606,7 @@ int vbf_filter_stream_record(vbf_filter* f, void* stream) {
     if (rc) return rc;
     if (s.host()) return host_resident("vbf_filter_stream_record");
     DEVICE_SCOPE(s.device);
+    s.pristine = false;
     if ((rc = storage_mark(s, (hipStream_t)stream))) return rc;
     if ((rc = mirror_after_write(s, (hipStream_t)stream))) return rc;
     return ok();
@@ -1702,6 +1713,7 @@ int vbf_filter_clear(vbf_filter* f, vbf_filter** out) {
                 s.mirror_ok = true;
             }
         }
+        s.pristine = true;
         device = s.device;
     }
     return make_filter(device, s.m, f->k, f->p, out);
@@ -1742,6 +1754,7 @@ int vbf_filter_words_to_host(const vbf_filter* f, uint32_t* out, uint64_t nwords
 // Caller holds s.mu (drained).
 static int words_from_host_locked(Storage& s, const uint32_t* in) {
     if (!s.nwords) return VBF_OK;
+    s.pristine = false;
     if (s.host()) {
         std::memcpy(s.h_words.data(), in, s.nwords * 4);
         return VBF_OK;
@@ -1787,19 +1800,21 @@ int vbf_filter_migrate(vbf_filter* f, int device) {
     if (rc) return rc;
     if (device == s.device) return ok();
     std::vector<uint32_t> w;
+    const bool zeros = s.pristine;  // nothing to copy: the target gets zeroed words
     if (s.host()) {
         w.swap(s.h_words);
     } else {
         DEVICE_SCOPE(s.device);
         if ((rc = storage_sync(s))) return rc;
-        w.resize(s.nwords);
-        if (s.nwords) HIP_TRY(hipMemcpy(w.data(), s.d_words, s.nwords * 4, hipMemcpyDeviceToHost));
+        if (!zeros || device == VBF_DEVICE_HOST) w.resize(s.nwords);
+        if (s.nwords && !zeros) HIP_TRY(hipMemcpy(w.data(), s.d_words, s.nwords * 4, hipMemcpyDeviceToHost));
     }
     uint32_t* nd = nullptr;
     if (device != VBF_DEVICE_HOST && s.nwords) {
         DEVICE_SCOPE(device);
         hipError_t e = hipMalloc((void**)&nd, s.nwords * 4);
-        if (e == hipSuccess) e = hipMemcpy(nd, w.data(), s.nwords * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = zeros ? hipMemset(nd, 0, s.nwords * 4)
+                                       : hipMemcpy(nd, w.data(), s.nwords * 4, hipMemcpyHostToDevice);
         if (e != hipSuccess) {  // the filter stays where it was, bits intact
             if (nd) (void)hipFree(nd);
             if (s.host()) s.h_words.swap(w);
@@ -2046,6 +2061,7 @@ static int rebuild_locked(vbf_filter* f, Storage& s, const uint8_t* data, uint64
         if ((rc = storage_wait(s, st))) return rc;
         vbf::KeyBatch kb2 = uniform ? batch(d_keys, nullptr, 0, ulen, n, 1) : batch(d_keys, d_off, 0, 0, n, 1);
         s.mirror_ok = false;
+        s.pristine = false;
         if ((rc = do_build(kb2, s.m, f->k, s.d_words, VBF_BUILD_AUTO, true, st))) return rc;
         if ((rc = storage_mark(s, st))) return rc;
         if ((rc = mirror_after_write(s, st))) return rc;

@@ -338,15 +338,35 @@ __global__ __launch_bounds__(256) void k_transpose_u16_v(const uint16_t* in, uin
     }
 }
 
-void launch_transpose_u16_strided(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols,
-                                  uint32_t in_stride, uint32_t out_stride, hipStream_t s) {
+// Any strides (the fallback of launch_transpose_u16_strided): 64 x 64 tiles of u16 elements.
+__global__ __launch_bounds__(256) void k_transpose_u16_s(const uint16_t* in, uint16_t* out, uint32_t rows,
+                                                         uint32_t cols, uint32_t in_stride, uint32_t out_stride) {
+    __shared__ uint16_t t[64][65];
+    const uint32_t c0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+    const uint32_t tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (uint32_t y = ty; y < 64; y += 4) {
+        const uint32_t r = r0 + y, c = c0 + tx;
+        if (r < rows && c < cols) t[y][tx] = in[(uint64_t)r * in_stride + c];
+    }
+    __syncthreads();
+    for (uint32_t y = ty; y < 64; y += 4) {
+        const uint32_t c = c0 + y, r = r0 + tx;
+        if (r < rows && c < cols) out[(uint64_t)c * out_stride + r] = t[tx][y];
+    }
+}
+
+hipError_t launch_transpose_u16_strided(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols,
+                                        uint32_t in_stride, uint32_t out_stride, hipStream_t s) {
+    if (rows == 0 || cols == 0) return hipSuccess;
+    if (in_stride < cols || out_stride < rows) return hipErrorInvalidValue;
     const bool vec = in_stride % 8 == 0 && out_stride % 8 == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
                      (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    const dim3 grid((cols + 63) / 64, (rows + 63) / 64);
     if (vec)
-        hipLaunchKernelGGL(k_transpose_u16_v, dim3((cols + 63) / 64, (rows + 63) / 64), dim3(256), 0, s, in, out,
-                           rows, cols, in_stride, out_stride);
-    else if (in_stride == cols && out_stride == rows)
-        launch_transpose_u16(in, out, rows, cols, s);
+        hipLaunchKernelGGL(k_transpose_u16_v, grid, dim3(256), 0, s, in, out, rows, cols, in_stride, out_stride);
+    else
+        hipLaunchKernelGGL(k_transpose_u16_s, grid, dim3(256), 0, s, in, out, rows, cols, in_stride, out_stride);
+    return hipGetLastError();
 }
 
 // OR 8 packed indices (8 u16 low halves + their 8 nibbles) into the segment bitmap.
@@ -383,9 +403,9 @@ __device__ __forceinline__ void load8(const uint32_t* tile, uint32_t cp, uint32_
 //      coalesced (one u16 pair per lane for the wave's tiles) and handed to the 8-lane groups with
 //      ds_bpermute; data loads unconditional (idle lanes re-read their run's first 8 entries) so
 //      vmcnt waits stay exact; NG runs per 8-lane group per batch (VBF_K3 3: 1024 threads NG=4;
-//      4: 1024, NG=5; 5: 768, NG=6; 6: 768, NG=8).
+//      4: 1024, NG=5; 5: 768, NG=6; 6: 768, NG=8; 8: 1024, NG=6; NG=8 at 1024 spills).
 //   6: flattened chunks in the three-stage pipeline -- no lane idles on a short run (VBF_K3 10:
-//      NG=4, 11: NG=5).  0.95 vs 1.03 ms at k = 10 (31-entry runs), but at k = 19 (m = 1.9e9,
+//      NG=4, 11: NG=5, 12: NG=6).  0.95 vs 1.03 ms at k = 10 (31-entry runs), but at k = 19 (m = 1.9e9,
 //      ~11-entry runs) it is the one that keeps K3 from idling 5/6 of its lanes.
 //   Measured and dropped (tools/env_ab.sh): coalesced bounds in the two-stage loop (-3 %);
 //   raw buffer loads with out-of-range offsets for idle lanes (no duplicate requests): 0.92 ms,
@@ -806,7 +826,8 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         phase_end(kPhaseTileSort, s);
         phase_begin(kPhaseTranspose, s);
         pl.ntS = (ntiles + 7) & ~7u;
-        launch_transpose_u16_strided(ends, endsT, ntiles, pl.nseg, pl.nsegS, pl.ntS, s);
+        err = launch_transpose_u16_strided(ends, endsT, ntiles, pl.nseg, pl.nsegS, pl.ntS, s);
+        if (err != hipSuccess) return err;
         // several workgroups per segment when there are few segments (small m)
         pl.G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
         const bool merge = atomic_merge || pl.G > 1;
@@ -819,6 +840,8 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         const uint32_t k3v = pl.k3v ? pl.k3v : (pl.C / std::max(pl.nseg, 1u) < kShortRun ? 10u : 4u);
         auto k3 = k3v == 10 ? k_seg_or<6, kPBlock, 4>
                 : k3v == 11 ? k_seg_or<6, kPBlock, 5>
+                : k3v == 12 ? k_seg_or<6, kPBlock, 6>
+                : k3v == 8 ? k_seg_or<3, kPBlock, 6>
                 : k3v == 3 ? k_seg_or<3, kPBlock, 4>
                 : k3v == 5 ? k_seg_or<3, 768, 6>
                 : k3v == 6 ? k_seg_or<3, 768, 8>

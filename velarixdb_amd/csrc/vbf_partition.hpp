@@ -88,8 +88,8 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
 // K2 (vbf_partition.hip): ends[rows][cols] -> endsT[cols][rows], shared by build and probe.
 void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t s);
 // The same with row strides (in: in_stride, out: out_stride elements); both multiples of 8 and
-// 16-byte aligned buffers take a 16-byte-vector kernel.
-void launch_transpose_u16_strided(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols,
+// 16-byte aligned buffers take a 16-byte-vector kernel, any other strides an element kernel.
+hipError_t launch_transpose_u16_strided(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols,
                                   uint32_t in_stride, uint32_t out_stride, hipStream_t s);
 
 // Partitioned probe plan (vbf_probe_part.hip): KT keys per tile, C = KT * k entries, segments of

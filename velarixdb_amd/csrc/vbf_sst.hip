@@ -14,8 +14,10 @@
 //   k_sst_walk : stage the block in LDS (all of a lane's 16-byte loads in flight at once), walk
 //                its entry chain (a dependent chain of u32 reads out of LDS, wave-uniform, scalar
 //                control), write the entry starts (u16, 256 slots per block) and the count.  A
-//                malformed block (an entry crossing the block end, more than 256 entries, a
-//                block over 64 KiB, offsets out of order) sets the error word instead.
+//                malformed block (an entry crossing the block end, a block over 64 KiB, offsets
+//                out of order) sets the error word instead.  A block of more than 256 entries
+//                (never written by the reference: 4096 / 17 = 240) is walked on to its end and
+//                counted; its entry starts are not stored (the emit pass re-walks it).
 //   exclusive scan of the counts (hipcub) -> entry base E_b of every block; the block's key
 //                bytes start at G_b = start_b - 17 * E_b (all bytes before it are entries).
 //   k_sst_emit : stage the block again, no walk: lanes write the entry arrays (one lane per
@@ -159,6 +161,17 @@ __device__ __forceinline__ uint32_t walk_chain(const BlockView& v, uint32_t blen
         }
     }
     bad = p != blen ? (p < blen ? kSstErrDense : kSstErrCross) : 0;
+    if (bad == kSstErrDense) {  // more than 256 entries: count the rest (starts not recorded)
+        for (;;) {
+            const uint32_t L = blen - p >= 4 ? __builtin_amdgcn_readfirstlane(v.u32(p)) : 0x10000u;
+            p = L > 0xFFFFu ? 0x20000u : p + L + kEntryFixed;
+            lmin = std::min(lmin, L);
+            lmax = std::max(lmax, L);
+            ++n;
+            if (p >= blen) break;
+        }
+        bad = p != blen ? kSstErrCross : 0;
+    }
     (void)lane;
     return n;
 }
@@ -195,10 +208,22 @@ __device__ __forceinline__ uint32_t walk_chain_v(const BlockView& v, uint32_t bl
             if (p >= blen) break;
         }
     }
-    bad = p != blen ? (p < blen ? kSstErrDense : kSstErrCross) : 0;
-    uint32_t n = 0;
-    lmin = 0xFFFFFFFFu;
-    lmax = 0;
+    // more than 256 entries: walk on to the block end, counting (starts not recorded) and
+    // reducing the key-length range on the way
+    uint32_t extra = 0, emin = 0xFFFFFFFFu, emax = 0;
+    while (p < blen) {
+        const bool has4 = p + 4 <= blen;
+        const uint32_t raw = v.u32(has4 ? p : 0u);
+        const uint32_t L = has4 ? raw : 0x10000u;
+        emin = std::min(emin, L);
+        emax = std::max(emax, L);
+        p += std::min(L, 0x10000u) + kEntryFixed;
+        ++extra;
+    }
+    bad = p != blen ? kSstErrCross : 0;
+    uint32_t n = extra;
+    lmin = emin;
+    lmax = emax;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
         const bool live = pr[k] < blen;
@@ -230,7 +255,7 @@ __device__ __forceinline__ bool uniform_block(const View& v, uint32_t blen, uint
     const uint32_t L0 = v.u32(0);
     if (L0 > 0xFFFFu) return false;
     const uint32_t E = L0 + kEntryFixed;
-    if (blen % E != 0 || blen / E > kMaxEnt) return false;
+    if (blen % E != 0) return false;
     const uint32_t cnt = blen / E;
     bool ok = true;
 #pragma unroll
@@ -239,6 +264,7 @@ __device__ __forceinline__ bool uniform_block(const View& v, uint32_t blen, uint
         pr[k] = i < cnt ? i * E : 0xFFFFFFFFu;
         if (i < cnt) ok &= v.u32(i * E) == L0;
     }
+    for (uint32_t i = lane + 64 * 4; i < cnt; i += 64) ok &= v.u32(i * E) == L0;  // dense blocks
     if (__ballot(!ok)) return false;
     n = cnt;
     lmin = lmax = L0;
@@ -292,7 +318,7 @@ __global__ __launch_bounds__(64 * kSstWaves) void k_sst_walk(SstArgs a) {
     // Blocks whose keys all have one length need no starts: entry i is at i * (L + 17), which
     // is how the emit pass finds them (lmin == lmax), so the 512-byte start list is not written.
     uint16_t* out = a.pos + b * kMaxEnt;
-    if (lmin != lmax) {
+    if (lmin != lmax && n <= kMaxEnt) {
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k)
             if (lane + 64 * k < n) out[lane + 64 * k] = (uint16_t)pr[k];
@@ -319,12 +345,38 @@ __global__ __launch_bounds__(64 * kSstWaves) void k_sst_emit(SstArgs a) {
     uint16_t* ps = pos[wave];
     if (!uni) {
         const uint16_t* pin = a.pos + b * kMaxEnt;
-        for (uint32_t i = lane; i < n; i += 64) ps[i] = pin[i];
+        for (uint32_t i = lane; i < n && i < kMaxEnt; i += 64) ps[i] = pin[i];
     }
     const BlockView v = stage_block(a, s, blen, stage[wave], lane);  // its barrier covers ps too
     auto start = [&](uint32_t i) { return uni ? i * (L0 + kEntryFixed) : (uint32_t)ps[i]; };
     const uint64_t E = a.ebase[b];
     const uint64_t G = s - (uint64_t)kEntryFixed * E;  // key bytes before this block
+    const uint64_t K = blen - (uint64_t)kEntryFixed * n;  // this block's key bytes
+    if (!uni && n > kMaxEnt) {
+        // a block of more than 256 entries of mixed key lengths (hand-written files only): its
+        // starts were not stored, so re-walk the chain 64 entries at a time, lane u taking entry
+        // base + u, and copy the key bytes per entry
+        uint32_t p = 0;
+        for (uint32_t base = 0; base < n; base += 64) {
+            uint32_t mine = 0;
+            for (uint32_t u = 0; u < 64 && base + u < n; ++u) {
+                mine = lane == u ? p : mine;
+                p += v.u32(p) + kEntryFixed;
+            }
+            const uint32_t i = base + lane;
+            if (i >= n) continue;
+            const uint32_t q = mine, L = v.u32(q);
+            const uint64_t dst = G + q - (uint64_t)kEntryFixed * i;
+            if (a.offsets) a.offsets[E + i] = dst;
+            if (a.val_off) a.val_off[E + i] = v.u32(q + 4 + L);
+            if (a.created) a.created[E + i] = (uint64_t)v.u32(q + 8 + L) | ((uint64_t)v.u32(q + 12 + L) << 32);
+            if (a.tomb) a.tomb[E + i] = v.u8(q + 16 + L) == 1;
+            if (a.keys)
+                for (uint32_t t = 0; t < L; ++t) a.keys[dst + t] = (uint8_t)v.u8(q + 4 + t);
+        }
+        if (a.offsets && b + 1 == a.nblocks && lane == 0) a.offsets[E + n] = G + K;
+        return;
+    }
     for (uint32_t i = lane; i < n; i += 64) {
         const uint32_t q = start(i);
         const uint32_t L = v.u32(q);
@@ -333,7 +385,6 @@ __global__ __launch_bounds__(64 * kSstWaves) void k_sst_emit(SstArgs a) {
         if (a.created) a.created[E + i] = (uint64_t)v.u32(q + 8 + L) | ((uint64_t)v.u32(q + 12 + L) << 32);
         if (a.tomb) a.tomb[E + i] = v.u8(q + 16 + L) == 1;
     }
-    const uint64_t K = blen - (uint64_t)kEntryFixed * n;  // this block's key bytes
     if (a.offsets && b + 1 == a.nblocks && lane == 0) a.offsets[E + n] = G + K;
     if (!a.keys || K == 0) return;
     // Fixed-size entries whose key length is a multiple of 4 (the walk's fast-path layout, with
