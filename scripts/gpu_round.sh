@@ -68,6 +68,8 @@ for s in $STEPS; do
     pmctcc) (cd /tmp && run pmctcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum --output-format csv -d "$OUT/pmctcc" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     pmctcc19) (cd /tmp && run pmctcc19 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum --output-format csv -d "$OUT/pmctcc19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     pmctcp) (cd /tmp && run pmctcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum --output-format csv -d "$OUT/pmctcp" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    pmctcp19) (cd /tmp && run pmctcp19 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmctcp19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    pmctcp10) (cd /tmp && run pmctcp10 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmctcp10" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     prof)   (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 40 --warmup 5 --no-cpu-baseline) || exit $? ;;
   esac
 done
