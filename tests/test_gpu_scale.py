@@ -168,6 +168,12 @@ def test_config3_full_size_properties(vbf, ora):
     w_part = build(vbf, keys, off, 0, n, m, k, 2)
     w_atom = build(vbf, keys, off, 0, n, m, k, 1)
     assert torch.equal(w_part, w_atom)
+    del w_atom
+    # the benchmarked form (bench.py --config 3): fresh build into garbage, offsets layout
+    w_fresh = torch.randint(-2**31, 2**31 - 1, ((m + 31) // 32,), dtype=torch.int32, device=DEV)
+    build(vbf, keys, off, 0, n, m, k, 2 | FRESH, words=w_fresh)
+    assert torch.equal(w_fresh, w_part)
+    del w_fresh
     assert count(vbf, keys, off, 0, n, m, k, w_part) == n
     # 50M negatives: FPR near theory (fill^k) -- the reference's probabilistic contract
     nn = 50_000_000

@@ -113,9 +113,15 @@ def test_empty_and_malformed(vbf, ora):
     with pytest.raises(VbfError, match="malformed"):
         vbf.sst.load_entries(data[:-3], index)          # truncated last entry (UnexpectedEof)
     blocks = ora.sst_index_blocks(index)
-    bad = ora.sst_write(np.zeros(8, np.uint8), np.array([0, 8], np.uint64))[1]  # 1-block index
-    with pytest.raises(VbfError, match="malformed"):
-        vbf.sst.load_entries(data, bad)                 # block far larger than 8192 bytes
+    one = ora.sst_write(np.zeros(8, np.uint8), np.array([0, 8], np.uint64))[1]  # 1-block index
+    # the whole file as ONE block of 1000 entries (~47 KB): load_entries reads entries sequentially
+    # whatever the blocking (fs/mod.rs:275-332), and so does the decoder (dense-block path)
+    assert data.size < 65536
+    _same(vbf.sst.load_entries(data, one), ora.sst_decode(data))
+    big, bigidx, _ = _rand_sst(ora, 11, 3000, list(range(20, 60)))
+    assert big.size > 65535
+    with pytest.raises(VbfError, match="larger than 65535"):
+        vbf.sst.load_entries(big, one)                  # one block over the decoder's 64 KiB limit
     # an index offset pointing into the middle of an entry
     raw = bytearray(index.tobytes())
     L0 = int.from_bytes(raw[0:4], "little")
