@@ -70,6 +70,9 @@ for s in $STEPS; do
     pmctcp) (cd /tmp && run pmctcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_PENDING_STALL_CYCLES_sum --output-format csv -d "$OUT/pmctcp" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     pmctcp19) (cd /tmp && run pmctcp19 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmctcp19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     pmctcp10) (cd /tmp && run pmctcp10 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmctcp10" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
+    abc16)  run ab_c16 900 env AB_PARITY=1 AB_ENVS="VBF_C16=1 VBF_C16=0" bash tools/env_ab.sh ;;
+    abc16_19) run ab_c16_19 600 env AB_ENVS="VBF_C16=0 VBF_C16=1 VBF_C16=0 VBF_C16=1" AB_ARGS="--bits-per-key 19" bash tools/env_ab.sh ;;
+    abc16_5) run ab_c16_5 600 bash -c 'for e in 0 1 0 1; do VBF_C16=$e python bench.py --config 5 --keys 250000000 --steps 5 --warmup 1 --no-cpu-baseline --neg-keys 1000000 | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(\"C16=$e\", round(d[\"ms_per_step\"],3), \"ms\", round(d[\"build_kernel_ms\"],3))"; done' ;;
     prof)   (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 40 --warmup 5 --no-cpu-baseline) || exit $? ;;
   esac
 done

@@ -237,3 +237,54 @@ def test_memtable_latency_tool_runs_without_gpu():
     assert out.returncode == 0, out.stderr
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert (r["m"], r["k"]) == (9815, 19) and 0 < r["host"]["n_elements"] <= 20000
+
+
+def test_host_residency_async_sync_mirror_calls():
+    """Round-3 entry points on a host-resident filter, no GPU needed: set_host_async sets at once
+    (nothing to overlap with) and calls the release callback before returning; sync / busy are
+    trivially idle; the mirror mode is accepted (a host filter is its own mirror); the stream
+    bracketing of external device writers is rejected like the other device entry points."""
+    import ctypes
+    from velarixdb_amd import HOST, BloomFilter
+    from velarixdb_amd._lib import VBF_EINVAL, call, lib
+    from velarixdb_amd.keys import pack
+    keys = [b"as%05d" % i for i in range(2000)]
+    bf = BloomFilter(1e-3, 2000, device=HOST)
+    b = pack(keys)
+    released = []
+    CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    cb = CB(lambda ctx: released.append(ctx))
+    d, o = b.ptrs()
+    call("vbf_filter_set_host_async", bf._h, d, o, b.stride, b.n, 1, ctypes.cast(cb, ctypes.c_void_p), 5)
+    assert released == [5] and not bf.busy() and bf.no_of_elements == 2000
+    bf.sync()
+    assert bf.contains_many(keys).all()
+    bf.set_many_async(keys[:10])  # library-copy form
+    assert bf.no_of_elements == 2010
+    for mode in ("off", "lazy", "eager"):
+        bf.set_mirror(mode)
+    assert lib.vbf_filter_set_mirror(bf._h, 7) == VBF_EINVAL
+    assert lib.vbf_filter_stream_wait(bf._h, None) == VBF_EINVAL
+    assert lib.vbf_filter_stream_record(bf._h, None) == VBF_EINVAL
+    assert b"host-resident" in lib.vbf_last_error()
+    # a pristine host filter migrates to host (no-op) and its words stay zero
+    z = BloomFilter(1e-3, 1000, device=HOST)
+    z.migrate(HOST)
+    assert not z.words().any()
+
+
+def test_multi_probe_host_filters_rejected_and_bounds_checked():
+    """vbf_multi_probe_host takes device-resident filters (mirror or GPU path); host-resident ones
+    are rejected before anything runs, as are NULL filters."""
+    import ctypes
+    from velarixdb_amd import HOST, BloomFilter
+    from velarixdb_amd._lib import VBF_EINVAL, lib
+    from velarixdb_amd.keys import pack
+    f = BloomFilter(1e-3, 100, device=HOST)
+    b = pack([b"x"])
+    out = np.zeros(1, np.uint8)
+    handles = (ctypes.c_void_p * 1)(f._h.value)
+    d, o = b.ptrs()
+    assert lib.vbf_multi_probe_host(d, o, b.stride, 1, 1, 1, handles, None, None, out.ctypes.data) == VBF_EINVAL
+    nulls = (ctypes.c_void_p * 1)(None)
+    assert lib.vbf_multi_probe_host(d, o, b.stride, 1, 1, 1, nulls, None, None, out.ctypes.data) == VBF_EINVAL

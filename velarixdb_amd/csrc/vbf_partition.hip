@@ -43,6 +43,8 @@ struct PartPlan {
     uint32_t fresh;       // K3: the words hold no filter yet -- write the segment without reading it
     uint32_t nsegS;       // row stride of ends[tile][seg] (nseg rounded up to 8: 16-byte rows)
     uint32_t ntS;         // row stride of endsT[seg][tile] (tiles rounded up to 8)
+    uint32_t c16;         // K1's segment counters are u16 pairs (half the LDS: larger tiles)
+    uint32_t cnt_words;   // K1's counter words (a multiple of 4: the image stays 16-byte aligned)
     uint64_t m, mu, nwords;
 };
 
@@ -95,12 +97,43 @@ __device__ __forceinline__ void lds_add(lds_u32* p) {
 __device__ __forceinline__ uint32_t lds_add_rtn(lds_u32* p) {
     return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+__device__ __forceinline__ void lds_add(lds_u32* p, uint32_t v) {
+    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_add_rtn(lds_u32* p, uint32_t v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Segment counters of K1.  C16 = false: one u32 per segment.  C16 = true: two u16 per word
+// (segment s in half s & 1 of word s >> 1; no half ever carries into the other: every count and
+// start is < CP <= 65535), which halves the counters' LDS -- at k = 19 (1 812 segments) that buys
+// the tile the keys of a full third stash round, at k = 4 / m = 2^32 - 1 (4 096 segments) 8 KiB
+// of image.  The half of segment s is bit 20 of the index: shift = (idx >> 16) & 16.
+template <bool C16>
+__device__ __forceinline__ void seg_count(lds_u32* cnt0, uint32_t idx) {
+    if constexpr (C16) lds_add(&cnt0[idx >> (kSegBits + 1)], 1u << ((idx >> (kSegBits - 4)) & 16u));
+    else lds_add(&cnt0[idx >> kSegBits]);
+}
+template <bool C16>
+__device__ __forceinline__ uint32_t seg_rank(lds_u32* cnt0, uint32_t idx) {
+    if constexpr (C16) {
+        const uint32_t sh = (idx >> (kSegBits - 4)) & 16u;
+        return (lds_add_rtn(&cnt0[idx >> (kSegBits + 1)], 1u << sh) >> sh) & 0xFFFFu;
+    } else {
+        return lds_add_rtn(&cnt0[idx >> kSegBits]);
+    }
+}
+template <bool C16>
+__device__ __forceinline__ uint32_t seg_get(const uint32_t* cnt, uint32_t s) {
+    if constexpr (C16) return (cnt[s >> 1] >> ((s & 1u) * 16)) & 0xFFFFu;
+    else return cnt[s];
+}
 
 // K > 0: k known at compile time (the stash and seed loops unroll, no indexed register moves);
 // K == 0: any k <= kStash at run time.  __launch_bounds__(1024, 8): two workgroups per CU (the
 // hashing of one overlaps the other's sort), i.e. at most 64 VGPRs; the offsets-layout kernels
 // would otherwise take 80-90 and drop to one workgroup per CU.
-template <int FMT, bool LP, int K, bool M31>
+template <int FMT, bool LP, int K, bool M31, bool C16 = false>
 __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan pl, uint32_t* tiles,
                                                        uint16_t* ends) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
@@ -109,11 +142,12 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     // atomics address them through an LDS-space pointer to 0, so a counter's address is the
     // segment number times 4 with no base to add -- one VALU instruction fewer per bit index in
     // each of the two passes.  Then the tile image, 16-byte aligned.
-    uint32_t* cnt = smem_all;                           // nseg_pad
+    uint32_t* cnt = smem_all;                           // nseg_pad (C16: nseg_pad / 2) words
     lds_u32* const cnt0 = reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(0));  // == cnt
-    uint32_t* wsum = cnt + pl.nseg_pad;                 // 16
+    const uint32_t cnt_words = pl.cnt_words;
+    uint32_t* wsum = cnt + cnt_words;                   // 16
     uint32_t* lhist = wsum + 16;                        // kLenBuckets (offsets layout)
-    uint32_t* smem = lhist + kLenBuckets;               // the image: (nseg_pad + 48) * 4 % 16 == 0
+    uint32_t* smem = lhist + kLenBuckets;               // the image: (cnt_words + 48) * 4 % 16 == 0
     uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // CP entries
     uint32_t* hi = smem + pl.CP / 2;                    // CP/8 words, 8 nibbles each
     const uint32_t tid = threadIdx.x;
@@ -123,7 +157,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     if (blockIdx.x >= pl.stagger_lo && blockIdx.x < pl.stagger_hi) {
         for (uint32_t i = 0; i < pl.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
     }
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
+    for (uint32_t s = tid; s < cnt_words; s += kPBlock) cnt[s] = 0;
     for (uint32_t w = tid; w < pl.CP / 8; w += kPBlock) hi[w] = 0;
     if (FMT < 0 && tid < kLenBuckets) lhist[tid] = 0;
     __syncthreads();
@@ -197,7 +231,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
                 if (valid && (SPL == 1 || seed0 + i < (uint32_t)K)) {
                     const uint64_t h = FMT > 0 ? seed_hash(q, seed0 + i) : prefix_hash(p, seed0 + i);
                     idx = mod_m<M31>(h, pl.m, pl.mu);
-                    lds_add(&cnt0[idx >> kSegBits]);
+                    seg_count<C16>(cnt0, idx);
                 }
                 stash[r * KL + i] = idx;
             }
@@ -217,14 +251,15 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
-                    lds_add(&cnt0[idx >> kSegBits]);
+                    seg_count<C16>(cnt0, idx);
                 }
                 stash[ns++] = idx;
             }
         }
     }
     __syncthreads();
-    block_exclusive_scan<true>(cnt, pl.nseg, wsum);  // starts of even-length runs
+    if constexpr (C16) block_exclusive_scan16<true>(cnt, pl.nseg, wsum);  // starts of even-length runs
+    else block_exclusive_scan<true>(cnt, pl.nseg, wsum);
     __syncthreads();
     if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
         uint32_t acc = 0;
@@ -242,7 +277,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? lds_add_rtn(&cnt0[val[q] >> kSegBits]) : 0u;
+            pos[q] = val[q] != kSentinel ? seg_rank<C16>(cnt0, val[q]) : 0u;
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -256,7 +291,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     // cnt[s] = start(s) + count(s) with every start even: an odd cnt marks an odd run, padded
     // with a copy of its last index.
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) {
-        const uint32_t c = cnt[s];
+        const uint32_t c = seg_get<C16>(cnt, s);
         if (c & 1u) {
             lo[c] = lo[c - 1];
             const uint32_t nib = (hi[(c - 1) >> 3] >> (((c - 1) & 7) * 4)) & 15u;
@@ -264,7 +299,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
         }
     }
     __syncthreads();
-    const uint32_t total = (cnt[pl.nseg - 1] + 1) & ~1u;
+    const uint32_t total = (seg_get<C16>(cnt, pl.nseg - 1) + 1) & ~1u;
     uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.tile_words;
     const uint32_t lo_words = total / 2;
     for (uint32_t w = tid * 4; w < lo_words; w += kPBlock * 4) {
@@ -277,7 +312,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     const uint32_t hi_words = (total + 7) / 8;
     for (uint32_t w = tid; w < hi_words; w += kPBlock) out_hi[w] = hi[w];
     uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nsegS;
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)((cnt[s] + 1) & ~1u);
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)((seg_get<C16>(cnt, s) + 1) & ~1u);
 }
 
 // ends[rows][cols] -> endsT[cols][rows], 64x64 tiles through LDS.
@@ -696,9 +731,14 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     const bool ck = k == 4 || k == 9 || k == 10 || k == 19;
     const uint32_t rmax = (uint32_t)(ck ? build_rounds_max((int)k, fixed) : rounds_max((int)k));
     const uint32_t kpr = kPBlock / (uint32_t)(ck ? build_spl((int)k, fixed) : 1);  // keys per round
+    // packed u16 counters where they buy tile (VBF_C16 = 0 / 1 forces them off / on: A/B)
+    static const int c16env = [] { const char* e = getenv("VBF_C16"); return e ? atoi(e) : -1; }();
+    pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) && (c16env >= 0 ? c16env != 0 : (k == 19 || k == 4)));
+    const uint32_t cnt_words = pl.c16 ? ((pl.nseg + 7) & ~7u) / 2 : pl.nseg_pad;
+    pl.cnt_words = cnt_words;
     for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
-        const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)pl.nseg_pad;
+        const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)cnt_words;
         // LDS = 2.5 * CP with CP <= C + nseg + 8
         const int64_t cmax = avail * 2 / 5 - pl.nseg - 8;
         const int64_t kt = std::min<int64_t>((int64_t)rmax * kpr, cmax / k);
@@ -712,7 +752,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     pl.CP = (pl.C + pl.nseg + 7) & ~7u;
     pl.tile_words = pl.CP / 2 + pl.CP / 8;
     pl.nsegS = (pl.nseg + 7) & ~7u;
-    pl.lds1 = (pl.CP / 2 + pl.CP / 8 + pl.nseg_pad + 16 + kLenBuckets) * 4;
+    pl.lds1 = (pl.CP / 2 + pl.CP / 8 + cnt_words + 16 + kLenBuckets) * 4;
     // VBF_TILE_LDS_MIN (experiments, speed only): request at least this much LDS per k_tile_pack
     // workgroup, e.g. > 80 KiB to hold one workgroup per CU
     static const int lds_min = [] { const char* e = getenv("VBF_TILE_LDS_MIN"); return e ? atoi(e) : 0; }();
@@ -805,9 +845,9 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
             // m <= 2^31: the one-word remainder (fast_mod31); the runtime-k kernel keeps the general one
             auto pick = [&]<bool S>() {
-                return k == 10 ? k_tile_pack<FMT, LP, 10, S>
-                     : k == 4  ? k_tile_pack<FMT, LP, 4, S>
-                     : k == 19 ? k_tile_pack<FMT, LP, 19, S>
+                return k == 10 ? (pl.c16 ? k_tile_pack<FMT, LP, 10, S, true> : k_tile_pack<FMT, LP, 10, S>)
+                     : k == 4  ? (pl.c16 ? k_tile_pack<FMT, LP, 4, S, true> : k_tile_pack<FMT, LP, 4, S>)
+                     : k == 19 ? (pl.c16 ? k_tile_pack<FMT, LP, 19, S, true> : k_tile_pack<FMT, LP, 19, S>)
                      : k == 9  ? k_tile_pack<FMT, LP, 9, S>
                                : k_tile_pack<FMT, LP, 0, false>;
             };

@@ -85,6 +85,39 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
     }
 }
 
+// The same over u16 counts packed two per word (count of s = half s & 1 of v[s >> 1]), in place;
+// n <= 4 * kPBlock, every start must fit 16 bits (the caller's CP <= 65535).
+template <bool EVEN = false>
+__device__ __forceinline__ void block_exclusive_scan16(uint32_t* v, uint32_t n, uint32_t* wsum) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t loc[4];
+    uint32_t sum = 0;
+    const uint32_t w0 = tid * 2 < (n + 1) / 2 ? v[tid * 2] : 0u;
+    const uint32_t w1 = tid * 2 + 1 < (n + 1) / 2 ? v[tid * 2 + 1] : 0u;
+    const uint32_t raw[4] = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t c = tid * 4 + q < n ? raw[q] : 0u;
+        loc[q] = EVEN ? (c + 1) & ~1u : c;
+        sum += loc[q];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t before = lane < wave ? wsum[lane] : 0u;
+#pragma unroll
+    for (int o = 8; o; o >>= 1) before += __shfl_xor(before, o);
+    before = (uint32_t)__shfl((int)before, 0);
+    const uint32_t r0 = before + incl - sum, r1 = r0 + loc[0], r2 = r1 + loc[1], r3 = r2 + loc[2];
+    if (tid * 2 < (n + 1) / 2) v[tid * 2] = r0 | (r1 << 16);
+    if (tid * 2 + 1 < (n + 1) / 2) v[tid * 2 + 1] = r2 | (r3 << 16);
+}
+
 // K2 (vbf_partition.hip): ends[rows][cols] -> endsT[cols][rows], shared by build and probe.
 void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t s);
 // The same with row strides (in: in_stride, out: out_stride elements); both multiples of 8 and
