@@ -45,6 +45,10 @@ def make_parser():
     ap.add_argument("--sst", action="store_true", help="SST data.db decode + rebuild (8(f) row 2)")
     ap.add_argument("--compact", action="store_true", help="compaction merge + filter (8(f) row 3)")
     ap.add_argument("--multi", action="store_true", help="batched multi-SST probe (8(f) row 4)")
+    ap.add_argument("--fanout", action="store_true",
+                    help="the compaction loop (sized.rs:170-200): per-bucket builds, synchronous vs asynchronous")
+    ap.add_argument("--buckets", type=int, default=8)
+    ap.add_argument("--fanout-reuse", action="store_true", help="--fanout: no per-bucket materialisation")
     ap.add_argument("--memtable", action="store_true",
                     help="single-key set/contains latency on a memtable-size filter (mem.rs:207-230)")
     ap.add_argument("--strategy", type=int, default=0, help="0 auto, 1 atomic, 2 partitioned")
@@ -119,10 +123,10 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32
 
 # rocprofv3 names of the build's kernels, and the summary of the same command, per (key bytes, k)
 ROCPROF = {
-    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true>", "transpose": "k_transpose_u16_v",
-                "seg_or": "k_seg_or<3, 1024, 5>"}, "profiles/r02/bench_default_kernel_stats.csv"),
-    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true>", "transpose": "k_transpose_u16_v",
-                "seg_or": "k_seg_or<6, 1024, 4>"}, "profiles/r02/bench_k19_kernel_stats.csv"),
+    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true, true>", "transpose": "k_transpose_u16_v",
+                "seg_or": "k_seg_or<3, 1024, 5>"}, "profiles/r03/bench_default_kernel_stats.csv"),
+    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true, true>", "transpose": "k_transpose_u16_v",
+                "seg_or": "k_seg_or<6, 1024, 4>"}, "profiles/r03/bench_k19_kernel_stats.csv"),
 }
 
 
@@ -644,6 +648,72 @@ def bench_e2e(ctx, args):
             "link_floor_ms": link * 1e3}
 
 
+def bench_fanout(ctx, args):
+    """The compaction loop of compactors/sized.rs:170-200 as the patched bf.rs runs it
+    (INTEGRATION.md): per bucket the merged table's keys are materialised on the CPU (here: copied
+    into a freshly allocated packed buffer, the merge's output), then BloomFilter::new(fpr, n) and
+    build_filter_from_entries.  `sync`: the build is vbf_filter_set_host on a fixed device (returns
+    with the bits done); `async`: VBF_DEVICE_AUTO placement and vbf_filter_set_host_async with the
+    release callback (returns at once, so the next bucket's materialisation overlaps the GPU
+    build).  Each mode ends when every filter's words are fetched (the SST writes) and the words
+    of both modes are compared.  One GPU here: the overlap is host work vs one GPU's H2D + build;
+    with 8 GPUs, AUTO puts consecutive buckets on different GPUs."""
+    B, n, L = args.buckets, args.keys, 16
+    p = wl.fpr_for_bits_per_key(10)
+    from velarixdb_amd.keys import HostBatch
+    srcs = []
+    keys = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
+    for b in range(B):
+        call("vbf_gen_fixed_dev", wl.SEED_CFG4 + b, 0, n, L, vp(keys), ctx.sp)
+        srcs.append(keys.cpu().numpy())
+    del keys
+
+    def run(mode):
+        t0 = time.perf_counter()
+        filters, merge_s = [], 0.0
+        for b in range(B):
+            m0 = time.perf_counter()
+            if args.fanout_reuse:
+                buf = srcs[b]  # no materialisation: the builds alone
+            else:
+                buf = np.empty_like(srcs[b])
+                np.copyto(buf, srcs[b])  # the merged table's keys, packed
+            merge_s += time.perf_counter() - m0
+            hb = HostBatch(buf, None, L, n, 1)
+            if mode == "sync":
+                f = vbf.BloomFilter(p, n, device=ctx.local)
+                f.set_batch(hb)
+            else:
+                f = vbf.BloomFilter(p, n, device="host")  # new() keeps a fresh filter on the host
+                f.migrate("auto")  # build_filter_from_entries: the library places it (no bits copied)
+                f.set_many_async(hb, zero_copy=True)
+            filters.append(f)
+        t_loop = time.perf_counter() - t0
+        words = [f.words() for f in filters]  # the SST writes wait for their filter
+        return time.perf_counter() - t0, t_loop, merge_s, words
+
+    for _ in range(args.warmup):
+        run("sync")
+        run("async")
+    res = {}
+    for mode in ("sync", "async"):
+        ts = [run(mode) for _ in range(args.steps)]
+        i = int(np.argsort([t[0] for t in ts])[len(ts) // 2])
+        res[mode] = {"total_ms": ts[i][0] * 1e3, "loop_ms": ts[i][1] * 1e3, "materialise_ms": ts[i][2] * 1e3,
+                     "keys_per_s": B * n / ts[i][0], "words": ts[i][3]}
+    same = all(np.array_equal(a, b) for a, b in zip(res["sync"]["words"], res["async"]["words"]))
+    for mode in res:
+        del res[mode]["words"]
+    assert same, "async builds differ from the synchronous ones"
+    return {"metric": "compaction loop keys/s (materialise + new + build per bucket, then the SST writes)",
+            "value": res["async"]["keys_per_s"], "unit": "keys/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": res["async"]["total_ms"], "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "%d buckets x %dM x 16B host keys, 10 bits/key" % (B, n // 10**6)},
+            "modes": res, "async_words_equal_sync": same,
+            "speedup": res["sync"]["total_ms"] / res["async"]["total_ms"]}
+
+
 def bench_sst(ctx, args):
     """the lazy filter rebuild of range.rs:117-128 from a config-2 SST --
     data.db decode (fs/mod.rs:275-332) alone, and decode + build fused
@@ -869,6 +939,9 @@ def main():
         res = bench_e2e(ctx, args)
     elif args.memtable:
         res = bench_memtable(ctx, args)
+    elif args.fanout:
+        args.keys = args.keys or 12_500_000
+        res = bench_fanout(ctx, args)
     else:
         args.keys = args.keys or (100_000_000 if args.config == 2 else 50_000_000)
         res = bench_fixed(ctx, args)

@@ -47,6 +47,8 @@ for s in $STEPS; do
     e2e)    run bench_e2e 600 python bench.py --e2e --steps 5 --warmup 1 ;;
     e2efresh) run bench_e2e_fresh 600 python bench.py --e2e --e2e-fresh-out --steps 5 --warmup 1 ;;
     memtable) run bench_memtable 300 python bench.py --memtable ;;
+    fanout) run bench_fanout 600 python bench.py --fanout --steps 3 --warmup 1 ;;
+    fanoutab) run bench_fanout_ab 900 bash -c 'for a in "" "--fanout-reuse"; do for h in 1 0; do echo "== H2D_DIRECT=$h $a"; VBF_H2D_DIRECT=$h python bench.py --fanout --steps 3 --warmup 1 $a | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print({m: (round(v[\"total_ms\"],1), round(v[\"loop_ms\"],1), round(v[\"materialise_ms\"],1)) for m, v in d[\"modes\"].items()})"; done; done' ;;
     prof19) (cd /tmp && run prof19 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 20 --warmup 3 --no-cpu-baseline) || exit $? ;;
     profmulti) (cd /tmp && run profmulti 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmulti" -o run -- python3 "$ROOT/bench.py" --multi --steps 10 --warmup 2) || exit $? ;;
     dist2spawn) run bench_dist2_spawn 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;

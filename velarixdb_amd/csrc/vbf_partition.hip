@@ -106,9 +106,10 @@ __device__ __forceinline__ uint32_t lds_add_rtn(lds_u32* p, uint32_t v) {
 
 // Segment counters of K1.  C16 = false: one u32 per segment.  C16 = true: two u16 per word
 // (segment s in half s & 1 of word s >> 1; no half ever carries into the other: every count and
-// start is < CP <= 65535), which halves the counters' LDS -- at k = 19 (1 812 segments) that buys
-// the tile the keys of a full third stash round, at k = 4 / m = 2^32 - 1 (4 096 segments) 8 KiB
-// of image.  The half of segment s is bit 20 of the index: shift = (idx >> 16) & 16.
+// start is < CP <= 65535), which halves the counters' LDS -- at k = 10 (954 segments) the tile
+// then holds its three full stash rounds (3 072 keys instead of 3 020), at k = 19 (1 812
+// segments) likewise (1 536 instead of 1 472).  The half of segment s is bit 20 of the index:
+// shift = (idx >> 16) & 16.
 template <bool C16>
 __device__ __forceinline__ void seg_count(lds_u32* cnt0, uint32_t idx) {
     if constexpr (C16) lds_add(&cnt0[idx >> (kSegBits + 1)], 1u << ((idx >> (kSegBits - 4)) & 16u));
@@ -733,7 +734,10 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     const uint32_t kpr = kPBlock / (uint32_t)(ck ? build_spl((int)k, fixed) : 1);  // keys per round
     // packed u16 counters where they buy tile (VBF_C16 = 0 / 1 forces them off / on: A/B)
     static const int c16env = [] { const char* e = getenv("VBF_C16"); return e ? atoi(e) : -1; }();
-    pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) && (c16env >= 0 ? c16env != 0 : (k == 19 || k == 4)));
+    // measured (profiles/r03/ab_c16*.log): k = 10 +1 % (tiles of 3 020 -> 3 072 keys: full stash
+    // rounds, fewer runs), k = 19 and k = 4 even (the extra VALU of the packed counters eats the
+    // larger tiles' gain)
+    pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) && (c16env >= 0 ? c16env != 0 : (k == 10 || k == 19)));
     const uint32_t cnt_words = pl.c16 ? ((pl.nseg + 7) & ~7u) / 2 : pl.nseg_pad;
     pl.cnt_words = cnt_words;
     for (uint32_t per_cu : {2u, 1u}) {

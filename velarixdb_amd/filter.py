@@ -61,6 +61,19 @@ def num_hash_functions(m, n):
     return int(lib.vbf_num_hash_functions(m, n & 0xFFFFFFFF))
 
 
+# zero-copy asynchronous sets: the batches the library still reads, released by its worker
+_INFLIGHT = {}
+_INFLIGHT_IDS = __import__("itertools").count(1)
+
+
+@ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+def _release(ctx):
+    _INFLIGHT.pop(ctx, None)
+
+
+_RELEASE_PTR = ctypes.cast(_release, ctypes.c_void_p)
+
+
 def _raise(fn, exc):
     code = exc.code
     if code == VBF_EDIVZERO:
@@ -199,14 +212,23 @@ class BloomFilter:
     def set_many(self, keys):
         self.set_batch(keys if isinstance(keys, HostBatch) else pack(keys))
 
-    def set_many_async(self, keys):
-        """set_many that returns before the GPU work is done (vbf_filter_set_host_async; the
-        library copies the keys first).  Later calls on the filter wait for it; sync() waits."""
+    def set_many_async(self, keys, zero_copy=False):
+        """set_many that returns before the GPU work is done (vbf_filter_set_host_async).  Later
+        calls on the filter wait for it; sync() waits.  By default the library copies the keys
+        first; zero_copy=True hands it the batch's own buffers instead, kept alive here until the
+        library's release callback (as a Rust caller hands over its packed Vec)."""
         b = keys if isinstance(keys, HostBatch) else pack(keys)
         d, o = b.ptrs()
+        rel, ctx = None, None
+        if zero_copy:
+            token = next(_INFLIGHT_IDS)
+            _INFLIGHT[token] = b
+            rel, ctx = _RELEASE_PTR, token
         try:
-            call("vbf_filter_set_host_async", self._h, d, o, b.stride, b.n, b.len_prefix, None, None)
+            call("vbf_filter_set_host_async", self._h, d, o, b.stride, b.n, b.len_prefix, rel, ctx)
         except VbfError as e:
+            if zero_copy:
+                _INFLIGHT.pop(ctx, None)
             _raise("set", e)
 
     def sync(self):
