@@ -449,6 +449,64 @@ def test_variable_length_knobs_same_words(vbf, ora, tmp_path):
             assert np.array_equal(np.load(stem + "_%d.npy" % k), want[k]), (lo, st, m, k)
 
 
+def test_partitioned_build_knobs_same_words(vbf, ora, tmp_path):
+    """The speed-only knobs of the fixed-length partitioned build -- VBF_K1 (the 1024-thread K1 with
+    two lanes per key at k = 19, or the 512-thread one-lane-per-key shape), VBF_ENDS_T (K1 writes
+    the run ends transposed, or the transpose kernel does), VBF_K3 (k_seg_or's tile loops: two-stage,
+    three-stage with 8-lane groups and its >8-group tail, flattened groups) -- must give the
+    oracle's words in every combination, on random keys and on a batch whose runs are thousands of
+    entries long (three keys repeated).  Each combination builds in a child process (the library
+    reads the knobs once per process)."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    from velarixdb_amd.keys import pack_fixed
+    # m = 2_999_999_999 has > 2048 segments: the 512-thread shape does not apply, V = 0 runs
+    cases = ((3_800_017, 19), (10_000_000, 10), (2_999_999_999, 19), (40_000_003, 10))
+    rng = np.random.default_rng(77)
+    rand = rng.integers(0, 256, (700_000, 16), dtype=np.uint8)
+    hot = rng.integers(0, 256, (3, 16), dtype=np.uint8)
+    rows = np.concatenate([rand, np.repeat(hot, 150_000, axis=0)])
+    np.save(tmp_path / "rows.npy", rows)
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import numpy as np, velarixdb_amd as v\n"
+        "from velarixdb_amd.keys import pack_fixed\n"
+        "b = pack_fixed(np.load(sys.argv[2]))\n"
+        "for m, k in %r:\n"
+        "    w = np.zeros((m + 31) // 32, np.uint32)\n"
+        "    v._lib.call('vbf_build_host', b.data.ctypes.data, None, 16, b.n, 1, m, k, w.ctypes.data, w.size, 0)\n"
+        "    nz = np.flatnonzero(w)\n"
+        "    np.save(sys.argv[1] + '_%%d_%%d.npy' %% (m, k), np.stack([nz.astype(np.uint64), w[nz].astype(np.uint64)]))\n"
+        "print('ok')\n" % (ROOT, cases))
+    b = pack_fixed(rows)
+    want = {}
+    for m, k in cases:
+        if m > 100_000_000:  # compare set-bit positions only (the words array is 375 MB)
+            want[(m, k)] = np.unique((ora.hashes(b, k) % np.uint64(m)).ravel())
+        else:
+            want[(m, k)] = ora.build_words(b, m, k, threads=8)
+    combos = (("0", "0", "0"), ("1", "1", "0"), ("1", "0", "3"), ("0", "1", "1"), ("1", "1", "4"),
+              ("-1", "1", "12"), ("0", "0", "10"))
+    for k1, et, k3 in combos:
+        env = {kk: vv for kk, vv in os.environ.items() if kk != "VBF_LIB"}
+        env["VBF_K1"], env["VBF_ENDS_T"], env["VBF_K3"] = k1, et, k3
+        stem = str(tmp_path / ("w%s%s%s" % (k1, et, k3)))
+        r = subprocess.run([sys.executable, "-c", code, stem, str(tmp_path / "rows.npy")], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "ok" in r.stdout, (k1, et, k3, r.stderr[-2000:])
+        for m, k in cases:
+            nz, val = np.load(stem + "_%d_%d.npy" % (m, k))  # the child's nonzero words
+            if m > 100_000_000:
+                bits = np.unpackbits(val.astype(np.uint32).view(np.uint8), bitorder="little").reshape(-1, 32)
+                idx = np.sort((nz[:, None] * np.uint64(32) + np.arange(32, dtype=np.uint64))[bits.astype(bool)])
+                assert np.array_equal(idx, want[(m, k)]), (k1, et, k3, m, k)
+            else:
+                got = np.zeros((m + 31) // 32, np.uint32)
+                got[nz.astype(np.int64)] = val.astype(np.uint32)
+                assert np.array_equal(got, want[(m, k)]), (k1, et, k3, m, k)
+
+
 @pytest.mark.parametrize("strategy", [1, 2])
 def test_concentrated_indices(vbf, ora, strategy):
     """Adversarial skew: 3M copies of three keys put every tile's 30K bit indices into a handful of

@@ -9,15 +9,17 @@
 //                    segment in LDS, scans the counts, and places every index into an LDS copy
 //                    of the tile sorted by segment.  The copy is PACKED: an index inside its
 //                    segment is 20 bits, stored as a u16 low half plus a 4-bit nibble (2.5 B per
-//                    index instead of 4), and every segment's run is padded to an even length
-//                    (by repeating one of its indices: OR is idempotent) so that K3's loads stay
-//                    dword-aligned.  The tile and its per-segment run ends (u16) are written
-//                    out with coalesced stores.
+//                    index instead of 4), in 8-entry GROUPS of 20 bytes -- the 8 low halves, then
+//                    the group's 8 nibbles in one word -- so that a run's low halves and nibbles
+//                    share cache lines (k_seg_or's time follows the L2 requests it makes, one
+//                    per 128-byte line a run touches: group layout 1.7 lines per run at k = 10
+//                    against 2.6 with the nibbles in a separate area, tools/rdgroup).  The tile
+//                    and its per-segment run ends (u16) are written out with coalesced stores.
 //   K2 k_transpose : ends[tile][seg] -> endsT[seg][tile] so each segment reads one row.
-//   K3 k_seg_or    : one workgroup per segment (128 KiB of LDS): 8-lane groups read that
-//                    segment's run from every tile with 16-byte loads, all issued before the
-//                    first ds_or, then the segment's 32768 words are written with coalesced
-//                    stores (or merged with word atomics when several workgroups share it).
+//   K3 k_seg_or    : one workgroup per segment (128 KiB of LDS): lanes read that segment's run
+//                    from every tile one 20-byte group each, all issued before the first ds_or,
+//                    then the segment's 32768 words are written with coalesced stores (or
+//                    merged with word atomics when several workgroups share it).
 //
 // Results are bit-identical to the per-key atomic kernel (OR is order-independent); the build
 // ORs into the existing words (bf.rs:89 never clears bits).
@@ -31,9 +33,9 @@ struct PartPlan {
     uint32_t R;           // hashing rounds per lane (ceil(KT / 1024))
     uint32_t KT;          // keys per tile
     uint32_t C;           // indices per tile (KT * k)
-    uint32_t CP;          // padded capacity: C + nseg, rounded up to a multiple of 8
+    uint32_t CP;          // capacity: C rounded up to a multiple of 8 (whole groups)
     uint32_t nseg, nseg_pad, G;
-    uint32_t tile_words;  // u32 words per tile in the workspace: CP/2 (lo16) + CP/8 (nibbles)
+    uint32_t tile_words;  // u32 words per tile in the workspace: 5 per group, rounded up to 4
     uint32_t lds1;        // K1 dynamic LDS bytes
     uint32_t stagger_lo, stagger_hi, stagger_sleeps;
     uint32_t ablate;      // ablation builds only (VBF_ABLATE, vbf_kernels.hpp): 1 skip place+copy
@@ -45,6 +47,8 @@ struct PartPlan {
     uint32_t ntS;         // row stride of endsT[seg][tile] (tiles rounded up to 8)
     uint32_t c16;         // K1's segment counters are u16 pairs (half the LDS: larger tiles)
     uint32_t cnt_words;   // K1's counter words (a multiple of 4: the image stays 16-byte aligned)
+    uint32_t k1v;         // K1's workgroup shape (k1_shape; VBF_K1)
+    uint32_t ends_t;      // K1 writes the run ends transposed, endsT[seg][tile] (VBF_ENDS_T)
     uint64_t m, mu, nwords;
 };
 
@@ -130,13 +134,22 @@ __device__ __forceinline__ uint32_t seg_get(const uint32_t* cnt, uint32_t s) {
     else return cnt[s];
 }
 
+// The packed tile image: entry e lives in group e >> 3, 20 bytes = 5 words: words 0..3 hold the
+// group's eight u16 low halves (entry e at u16 (e >> 3) * 10 + (e & 7)), word 4 its eight 4-bit
+// nibbles (entry e at bits 4 * (e & 7)).
+constexpr uint32_t kGroupWords = 5;
+__host__ __device__ constexpr uint32_t group_words(uint32_t entries) { return (entries + 7) / 8 * kGroupWords; }
+
 // K > 0: k known at compile time (the stash and seed loops unroll, no indexed register moves);
-// K == 0: any k <= kStash at run time.  __launch_bounds__(1024, 8): two workgroups per CU (the
-// hashing of one overlaps the other's sort), i.e. at most 64 VGPRs; the offsets-layout kernels
-// would otherwise take 80-90 and drop to one workgroup per CU.
-template <int FMT, bool LP, int K, bool M31, bool C16 = false>
-__global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan pl, uint32_t* tiles,
-                                                       uint16_t* ends) {
+// K == 0: any k <= kStash at run time.  V = 0: __launch_bounds__(1024, 8): two workgroups per CU
+// (the hashing of one overlaps the other's sort), i.e. at most 64 VGPRs; the offsets-layout
+// kernels would otherwise take 80-90 and drop to one workgroup per CU.  V = 1: 512 threads, two
+// workgroups per CU at 4 waves per SIMD, 128 VGPRs (k1_shape).
+template <int FMT, bool LP, int K, bool M31, bool C16 = false, int V = 0>
+__global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile_pack(DevKeys dk, PartPlan pl,
+                                                                                      uint32_t* tiles, uint16_t* ends) {
+    constexpr int BS = V == 1 ? 512 : kPBlock;  // k1_shape(K, FMT > 0, V).bs
+    static_assert(V == 0 || (K > 0 && FMT > 0), "the 512-thread shape is for compiled k and fixed-length keys");
     extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
     // The per-segment counters first, at LDS address 0 (the kernel has no static LDS, so the
     // dynamic allocation starts there; launch_build_partitioned checks it): the count and rank
@@ -149,8 +162,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     uint32_t* wsum = cnt + cnt_words;                   // 16
     uint32_t* lhist = wsum + 16;                        // kLenBuckets (offsets layout)
     uint32_t* smem = lhist + kLenBuckets;               // the image: (cnt_words + 48) * 4 % 16 == 0
-    uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // CP entries
-    uint32_t* hi = smem + pl.CP / 2;                    // CP/8 words, 8 nibbles each
+    uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // before placement: perm (offsets layout)
     const uint32_t tid = threadIdx.x;
     // Stagger (speed only): the second workgroup dispatched to each CU starts ~half a tile
     // later, so the two co-resident workgroups alternate hashing (VALU) and sorting (LDS)
@@ -158,19 +170,26 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     if (blockIdx.x >= pl.stagger_lo && blockIdx.x < pl.stagger_hi) {
         for (uint32_t i = 0; i < pl.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
     }
-    for (uint32_t s = tid; s < cnt_words; s += kPBlock) cnt[s] = 0;
-    for (uint32_t w = tid; w < pl.CP / 8; w += kPBlock) hi[w] = 0;
+    for (uint32_t s = tid; s < cnt_words; s += BS) cnt[s] = 0;
     if (FMT < 0 && tid < kLenBuckets) lhist[tid] = 0;
     __syncthreads();
 
-    // SPL lanes per key (build_spl): lane tid takes key slot r * (kPBlock / SPL) + tid / SPL and
+    // SPL lanes per key (k1_shape): lane tid takes key slot r * (BS / SPL) + tid / SPL and
     // seeds [KL * (tid % SPL), KL * (tid % SPL) + KL) of it
-    constexpr int SPL = K > 0 ? build_spl(K, FMT > 0) : 1;
-    constexpr int KL = K > 0 ? build_kl(K, FMT > 0) : 1;
-    constexpr uint32_t kKeysPerRound = kPBlock / SPL;
-    constexpr int RMK = K > 0 ? build_rounds_max(K, FMT > 0) : 1;
+    constexpr int SPL = K > 0 ? k1_shape(K, FMT > 0, V).spl : 1;
+    constexpr int KL = K > 0 ? k1_shape(K, FMT > 0, V).kl : 1;
+    constexpr uint32_t kKeysPerRound = BS / SPL;
+    constexpr int RMK = K > 0 ? k1_shape(K, FMT > 0, V).rounds : 1;
     uint32_t stash[K > 0 ? RMK * KL : kStash];
-    const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
+    // the tile: with ends_t, XCD-aware (blocks are dealt round-robin over the 8 XCDs; each XCD
+    // takes a contiguous range of tiles, so the endsT columns its workgroups write at one time are
+    // neighbours and fill whole L2 lines); otherwise the block number
+    uint32_t tile = blockIdx.x;
+    if (pl.ends_t) {
+        const uint32_t nwg = gridDim.x, q = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+        tile = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + blockIdx.x / 8;
+    }
+    const uint64_t key0 = (uint64_t)tile * pl.KT;
     const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
     const uint32_t nk = (uint32_t)(key_end - key0);
     // perm lives in the (not yet used) tile image; every read of it precedes the barrier below
@@ -244,7 +263,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
     } else {
         ns = 0;
         for (uint32_t r = 0; r < pl.R; ++r) {
-            const uint32_t slot = r * kPBlock + tid;
+            const uint32_t slot = r * BS + tid;
             const bool valid = slot < nk;
             Prefix p{};
             if (valid) p = key_prefix<FMT, LP>(dk, key_of(slot));
@@ -259,8 +278,11 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
         }
     }
     __syncthreads();
-    if constexpr (C16) block_exclusive_scan16<true>(cnt, pl.nseg, wsum);  // starts of even-length runs
-    else block_exclusive_scan<true>(cnt, pl.nseg, wsum);
+    if constexpr (C16) block_exclusive_scan16(cnt, pl.nseg, wsum);  // run starts
+    else block_exclusive_scan(cnt, pl.nseg, wsum);
+    // the groups' nibble words start clear (ORed into below); the image held perm / staged keys
+    // until the hashing rounds ended
+    for (uint32_t g = tid; g < pl.CP / 8; g += BS) smem[g * kGroupWords + 4] = 0;
     __syncthreads();
     if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
         uint32_t acc = 0;
@@ -283,37 +305,30 @@ __global__ __launch_bounds__(kPBlock, 8) void k_tile_pack(DevKeys dk, PartPlan p
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (val[q] != kSentinel) {
-                lo[pos[q]] = (uint16_t)val[q];
-                atomicOr(&hi[pos[q] >> 3], ((val[q] >> 16) & kNibMask) << ((pos[q] & 7) * 4));
+                const uint32_t g = (pos[q] >> 3) * kGroupWords, e7 = pos[q] & 7;
+                lo[g * 2 + e7] = (uint16_t)val[q];
+                atomicOr(&smem[g + 4], ((val[q] >> 16) & kNibMask) << (e7 * 4));
             }
         }
     }
     __syncthreads();
-    // cnt[s] = start(s) + count(s) with every start even: an odd cnt marks an odd run, padded
-    // with a copy of its last index.
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) {
-        const uint32_t c = seg_get<C16>(cnt, s);
-        if (c & 1u) {
-            lo[c] = lo[c - 1];
-            const uint32_t nib = (hi[(c - 1) >> 3] >> (((c - 1) & 7) * 4)) & 15u;
-            atomicOr(&hi[c >> 3], nib << ((c & 7) * 4));
-        }
-    }
-    __syncthreads();
-    const uint32_t total = (seg_get<C16>(cnt, pl.nseg - 1) + 1) & ~1u;
-    uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.tile_words;
-    const uint32_t lo_words = total / 2;
-    for (uint32_t w = tid * 4; w < lo_words; w += kPBlock * 4) {
-        if (w + 4 <= lo_words)
+    // cnt[s] = start(s) + count(s) = the end of segment s's run.  The last group's low halves past
+    // the tile's end are whatever LDS held: every reader masks entries by the run bounds.
+    const uint32_t total = seg_get<C16>(cnt, pl.nseg - 1);
+    uint32_t* out = tiles + (uint64_t)tile * pl.tile_words;
+    const uint32_t words = group_words(total);
+    for (uint32_t w = tid * 4; w < words; w += BS * 4) {
+        if (w + 4 <= words)
             *reinterpret_cast<uint4*>(out + w) = *reinterpret_cast<const uint4*>(smem + w);
         else
-            for (uint32_t x = w; x < lo_words; ++x) out[x] = smem[x];
+            for (uint32_t x = w; x < words; ++x) out[x] = smem[x];
     }
-    uint32_t* out_hi = out + pl.CP / 2;
-    const uint32_t hi_words = (total + 7) / 8;
-    for (uint32_t w = tid; w < hi_words; w += kPBlock) out_hi[w] = hi[w];
-    uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nsegS;
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) eo[s] = (uint16_t)((seg_get<C16>(cnt, s) + 1) & ~1u);
+    if (pl.ends_t) {  // straight into endsT[seg][tile] (no transpose pass)
+        for (uint32_t s = tid; s < pl.nseg; s += BS) ends[(uint64_t)s * pl.ntS + tile] = (uint16_t)seg_get<C16>(cnt, s);
+    } else {
+        uint16_t* eo = ends + (uint64_t)tile * pl.nsegS;
+        for (uint32_t s = tid; s < pl.nseg; s += BS) eo[s] = (uint16_t)seg_get<C16>(cnt, s);
+    }
 }
 
 // ends[rows][cols] -> endsT[cols][rows], 64x64 tiles through LDS.
@@ -405,31 +420,36 @@ hipError_t launch_transpose_u16_strided(const uint16_t* in, uint16_t* out, uint3
     return hipGetLastError();
 }
 
-// OR 8 packed indices (8 u16 low halves + their 8 nibbles) into the segment bitmap.
-__device__ __forceinline__ void or8(uint32_t* bitmap, uint4 l, uint32_t nib, uint32_t valid, uint32_t abl = 0) {
+// OR entries [a, b) of one group (8 u16 low halves in l, their 8 nibbles in nib) into the segment
+// bitmap.
+__device__ __forceinline__ void or_group(uint32_t* bitmap, uint4 l, uint32_t nib, uint32_t a, uint32_t b,
+                                         uint32_t abl = 0) {
     if (abl == 3) {  // timing experiment: consume the loads without touching LDS
-        if ((l.x ^ l.y ^ l.z ^ l.w ^ nib) == 0x12345678u && valid == 9) bitmap[0] = 1;
+        if ((l.x ^ l.y ^ l.z ^ l.w ^ nib) == 0x12345678u && b == 9) bitmap[0] = a;
         return;
     }
     const uint32_t w[4] = {l.x, l.y, l.z, l.w};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-        if ((uint32_t)c < valid) {
+        if ((uint32_t)c >= a && (uint32_t)c < b) {
             const uint32_t idx = ((w[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) | (((nib >> (4 * c)) & 15u) << 16);
             atomicOr(&bitmap[idx >> 5], 1u << (idx & 31));
         }
     }
 }
 
-// Loads elements [e, e+8) of a packed tile: 16 bytes of low halves (e even -> dword aligned) and
-// the 8 nibbles from the two nibble words around e.  Bytes past the run belong to the same tile
-// or to the workspace's tail pad and are masked by the caller.
-__device__ __forceinline__ void load8(const uint32_t* tile, uint32_t cp, uint32_t e, uint4& l, uint32_t& nib) {
-    __builtin_memcpy(&l, tile + e / 2, 16);
-    uint2 h;
-    __builtin_memcpy(&h, tile + cp / 2 + (e >> 3), 8);
-    const uint64_t hh = ((uint64_t)h.y << 32) | h.x;
-    nib = (uint32_t)(hh >> ((e & 7) * 4));
+// Loads group g of a packed tile: 16 bytes of low halves and the nibble word after them (the group
+// is 4-byte aligned; bytes past the tile's last entry are masked by the caller).
+__device__ __forceinline__ void load_group(const uint32_t* tile, uint32_t g, uint4& l, uint32_t& nib) {
+    __builtin_memcpy(&l, tile + g * kGroupWords, 16);
+    nib = tile[g * kGroupWords + 4];
+}
+
+// Entries of group gi inside the run [st, en): [a, b) packed as a | b << 4 (0: none).
+__device__ __forceinline__ uint32_t group_range(uint32_t gi, uint32_t st, uint32_t en) {
+    if (gi * 8 >= en || gi * 8 + 8 <= st) return 0u;
+    const uint32_t a = gi * 8 < st ? st - gi * 8 : 0u, b = std::min<uint32_t>(8, en - gi * 8);
+    return a | (b << 4);
 }
 
 // K3 tile-loop variants (speed only; identical results).  By default the plan picks V3 (NG = 5)
@@ -437,16 +457,18 @@ __device__ __forceinline__ void load8(const uint32_t* tile, uint32_t cp, uint32_
 //   1: two-stage -- run bounds of batch b+1 (8 u16 loads per lane) in flight with batch b's data
 //   3: three-stage -- bounds of b+2, data of b+1 and the ORs of b overlap; run bounds loaded
 //      coalesced (one u16 pair per lane for the wave's tiles) and handed to the 8-lane groups with
-//      ds_bpermute; data loads unconditional (idle lanes re-read their run's first 8 entries) so
-//      vmcnt waits stay exact; NG runs per 8-lane group per batch (VBF_K3 3: 1024 threads NG=4;
-//      4: 1024, NG=5; 5: 768, NG=6; 6: 768, NG=8; 8: 1024, NG=6; NG=8 at 1024 spills).
-//   6: flattened chunks in the three-stage pipeline -- no lane idles on a short run (VBF_K3 10:
-//      NG=4, 11: NG=5, 12: NG=6).  0.95 vs 1.03 ms at k = 10 (31-entry runs), but at k = 19 (m = 1.9e9,
-//      ~11-entry runs) it is the one that keeps K3 from idling 5/6 of its lanes.
+//      ds_bpermute; lane q of a group reads the run's q-th group (and q+8, ... past 8 groups);
+//      data loads unconditional (idle lanes re-read their run's first group) so vmcnt waits stay
+//      exact; NG runs per 8-lane group per batch (VBF_K3 3: 1024 threads NG=4; 4: 1024, NG=5;
+//      5: 768, NG=6; 6: 768, NG=8; 8: 1024, NG=6; NG=8 at 1024 spills); VBF_K3 13: 4-lane groups,
+//      NG=4 (16 runs per load instruction, no idle lanes on short runs, no prefix search).
+//   6: flattened -- a wave's runs' groups dealt to lanes back to back, no lane idles on a short
+//      run (VBF_K3 10: NG=4, 11: NG=5, 12: NG=6).  At k = 19 (m = 1.9e9, ~16-entry runs) it is
+//      the one that keeps K3 from idling most of its lanes.
 //   Measured and dropped (tools/env_ab.sh): coalesced bounds in the two-stage loop (-3 %);
-//   raw buffer loads with out-of-range offsets for idle lanes (no duplicate requests): 0.92 ms,
-//   the same as the duplicates (the texture addresser coalesces them).
-template <int V, int BS = kPBlock, int NG = 8>
+//   raw buffer loads with out-of-range offsets for idle lanes (no duplicate requests): the same
+//   as the duplicates (the texture addresser coalesces them).
+template <int V, int BS = kPBlock, int NG = 8, int LPR = 8>
 __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint16_t* endsT,
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
                                                     uint32_t* words) {
@@ -480,21 +502,29 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
     const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / pl.G);
     const uint16_t* row_end = endsT + (uint64_t)seg * pl.ntS;
     const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * pl.ntS : nullptr;
-    const uint32_t grp = lane >> 3, q8 = (lane & 7) * 8;
-    // a wave serves 8 * NG tiles per batch (8-lane groups, NG runs each)
-    const uint32_t step = (BS / 64) * 8 * NG;
-    uint32_t tg = t_lo + wave * 8 * NG;
-    // runs longer than 64 indices (rare at the default plan; common for tiny m)
-    auto tail = [&](uint32_t t, uint32_t st, uint32_t len) {
+    // V 0 / 3: LPR-lane groups, one run each (RPW runs per wave per load instruction)
+    static_assert(LPR == 4 || LPR == 8, "lanes per run");
+    constexpr uint32_t RPW = 64 / LPR;
+    static_assert(V != 3 || RPW * NG <= 64, "one coalesced bounds load per batch covers 64 tiles");
+    static_assert(V != 0 || LPR == 8, "the two-stage loop deals 8-lane groups");
+    const uint32_t grp = lane / LPR, q8 = lane % LPR;
+    // a wave serves RPW * NG tiles per batch (NG runs per lane group)
+    const uint32_t step = (BS / 64) * RPW * NG;
+    uint32_t tg = t_lo + wave * RPW * NG;
+    const uint32_t abl = VBF_ABLATION_BUILD ? pl.ablate : 0u;
+    // groups LPR.. of a run that spans more than LPR (rare at the default plans; common for tiny m)
+    auto tail = [&](uint32_t t, uint32_t st, uint32_t en) {
         const uint32_t* tile = tiles + (uint64_t)t * pl.tile_words;
 #pragma unroll 1
-        for (uint32_t e = q8 + 64; e < len; e += 64) {
+        for (uint32_t gi = (st >> 3) + q8 + LPR; gi * 8 < en; gi += LPR) {
             uint4 lt;
             uint32_t nt;
-            load8(tile, pl.CP, st + e, lt, nt);
-            or8(bitmap, lt, nt, std::min<uint32_t>(8, len - e));
+            load_group(tile, gi, lt, nt);
+            const uint32_t ab = group_range(gi, st, en);
+            or_group(bitmap, lt, nt, ab & 15u, ab >> 4);
         }
     };
+    auto spans_more = [](uint32_t st, uint32_t en) { return en > st && ((en + 7) >> 3) - (st >> 3) > LPR; };
     // packed bounds (begin | end << 16) of tile tg + lane, one coalesced u16 pair per lane
     auto lb = [&](uint32_t t0) -> uint32_t {
         const uint32_t t = t0 + lane;
@@ -506,20 +536,21 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
     if (pl.ablate >= 5) {
         // 5-7: timing experiments, fixed costs only
     } else if constexpr (V == 6) {
-        // Flattened chunks for SHORT runs (large k or m: C / nseg entries per run): a wave's 64
-        // runs (one per tile, bounds in lane order) are cut into 8-entry chunks dealt to lanes
-        // back to back, so no lane idles on a short run.  A lane finds its run by a 6-step binary
-        // search over the wave's exclusive chunk prefix (ds_bpermute).  Pipelined like V3: the
-        // bounds of batch b+2, the chunk loads of batch b+1 and the ORs of batch b in flight
-        // together.  Chunks beyond NG * 64 per batch are loaded and ORed at consume time.
+        // Flattened groups for SHORT runs (large k or m: C / nseg entries per run): the groups of
+        // a wave's 64 runs (one per tile, bounds in lane order) are dealt to lanes back to back,
+        // so no lane idles on a short run.  A lane finds its run by a 6-step binary search over
+        // the wave's exclusive group prefix (ds_bpermute).  Pipelined like V3: the bounds of batch
+        // b+2, the group loads of batch b+1 and the ORs of batch b in flight together.  Groups
+        // beyond NG * 64 per batch are loaded and ORed at consume time.
         const uint32_t wstep = (BS / 64) * 64;
         struct FB {
             uint32_t v, excl, total;
             uint4 l[NG];
-            uint32_t nib[NG], cnt[NG];
+            uint32_t nib[NG], ab[NG];
         };
         auto prep = [&](uint32_t v, FB& b) {
-            const uint32_t ch = (((v >> 16) - (v & 0xFFFFu)) + 7) >> 3;
+            const uint32_t st = v & 0xFFFFu, en = v >> 16;
+            const uint32_t ch = en > st ? ((en + 7) >> 3) - (st >> 3) : 0u;
             uint32_t incl = ch;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -530,41 +561,41 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
             b.excl = incl - ch;
             b.total = (uint32_t)__shfl((int)incl, 63);
         };
-        // chunk c of the batch at t0 -> (tile, entry offset, live entries)
-        auto locate = [&](const FB& b, uint32_t t0, uint32_t c, const uint32_t*& tile, uint32_t& e) -> uint32_t {
+        // group c of the batch at t0 -> (tile, group index, live entries a | b << 4; 0 past the end)
+        auto locate = [&](const FB& b, uint32_t t0, uint32_t c, const uint32_t*& tile, uint32_t& gi) -> uint32_t {
             uint32_t r = 0;
 #pragma unroll
             for (int sft = 32; sft; sft >>= 1)
                 if ((uint32_t)__shfl((int)b.excl, (int)r + sft) <= c) r += sft;
             const uint32_t rv = (uint32_t)__shfl((int)b.v, (int)r), rex = (uint32_t)__shfl((int)b.excl, (int)r);
-            const uint32_t rst = rv & 0xFFFFu, rlen = (rv >> 16) - rst, off = (c - rex) * 8;
+            const uint32_t rst = rv & 0xFFFFu, ren = rv >> 16;
             tile = tiles + (uint64_t)std::min(t0 + r, t_hi - 1) * pl.tile_words;
-            e = rst + off;
-            return c < b.total ? std::min<uint32_t>(8, rlen - off) : 0u;
+            gi = (rst >> 3) + (c - rex);
+            return c < b.total ? group_range(gi, rst, ren) : 0u;
         };
         auto issue = [&](uint32_t t0, FB& b) {
 #pragma unroll
             for (int q = 0; q < NG; ++q) {
                 const uint32_t* tile;
-                uint32_t e;
-                b.cnt[q] = locate(b, t0, (uint32_t)q * 64 + lane, tile, e);
-                if (b.cnt[q]) load8(tile, pl.CP, e, b.l[q], b.nib[q]);
+                uint32_t gi;
+                b.ab[q] = locate(b, t0, (uint32_t)q * 64 + lane, tile, gi);
+                if (b.ab[q]) load_group(tile, gi, b.l[q], b.nib[q]);
             }
         };
         auto consume = [&](uint32_t t0, const FB& b) {
 #pragma unroll
             for (int q = 0; q < NG; ++q)
-                if (b.cnt[q]) or8(bitmap, b.l[q], b.nib[q], b.cnt[q]);
+                if (b.ab[q]) or_group(bitmap, b.l[q], b.nib[q], b.ab[q] & 15u, b.ab[q] >> 4, abl);
 #pragma unroll 1
             for (uint32_t c0 = 64 * NG; c0 < b.total; c0 += 64) {
                 const uint32_t* tile;
-                uint32_t e;
-                const uint32_t n8 = locate(b, t0, c0 + lane, tile, e);
-                if (n8) {
+                uint32_t gi;
+                const uint32_t ab = locate(b, t0, c0 + lane, tile, gi);
+                if (ab) {
                     uint4 lt;
                     uint32_t nt;
-                    load8(tile, pl.CP, e, lt, nt);
-                    or8(bitmap, lt, nt, n8);
+                    load_group(tile, gi, lt, nt);
+                    or_group(bitmap, lt, nt, ab & 15u, ab >> 4, abl);
                 }
             }
         };
@@ -597,33 +628,34 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
         };
         auto spread = [&](uint32_t v, Batch& b) {
 #pragma unroll
-            for (int g = 0; g < NG; ++g) b.be[g] = (uint32_t)__shfl((int)v, g * 8 + grp);
+            for (int g = 0; g < NG; ++g) b.be[g] = (uint32_t)__shfl((int)v, g * RPW + grp);
         };
         auto issue = [&](uint32_t t0, Batch& b) {
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
-                const uint32_t st = b.be[g] & 0xFFFFu, len = (b.be[g] >> 16) - st;
-                const uint32_t t = std::min(t0 + g * 8 + grp, t_hi - 1);
-                // idle lanes re-read the run's first 8 entries (same lines, always in bounds)
-                const uint32_t e = q8 < len ? st + q8 : st;
+                const uint32_t st = b.be[g] & 0xFFFFu, en = b.be[g] >> 16;
+                const uint32_t t = std::min(t0 + g * RPW + grp, t_hi - 1);
+                // idle lanes re-read the run's first group (same lines, always in bounds)
+                const uint32_t gi = ((st >> 3) + q8) * 8 < en ? (st >> 3) + q8 : st >> 3;
                 if (VBF_ABLATION_BUILD && pl.ablate == 4) {  // timing experiment: no tile loads
-                    b.l[g] = make_uint4(t * 2654435761u + g, lane * 40503u, t ^ lane, e * 977u);
+                    b.l[g] = make_uint4(t * 2654435761u + g, lane * 40503u, t ^ lane, gi * 977u);
                     b.nib[g] = t + lane;
                 } else {
-                    load8(tiles + (uint64_t)t * pl.tile_words, pl.CP, e, b.l[g], b.nib[g]);
+                    load_group(tiles + (uint64_t)t * pl.tile_words, gi, b.l[g], b.nib[g]);
                 }
             }
         };
         auto consume = [&](uint32_t t0, const Batch& b) {
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
-                const uint32_t st = b.be[g] & 0xFFFFu, len = (b.be[g] >> 16) - st;
-                if (q8 < len) or8(bitmap, b.l[g], b.nib[g], std::min<uint32_t>(8, len - q8), VBF_ABLATION_BUILD ? pl.ablate : 0);
+                const uint32_t st = b.be[g] & 0xFFFFu, en = b.be[g] >> 16;
+                const uint32_t ab = group_range((st >> 3) + q8, st, en);
+                if (ab) or_group(bitmap, b.l[g], b.nib[g], ab & 15u, ab >> 4, abl);
             }
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
-                const uint32_t st = b.be[g] & 0xFFFFu, len = (b.be[g] >> 16) - st;
-                if (len > 64) tail(t0 + g * 8 + grp, st, len);
+                const uint32_t st = b.be[g] & 0xFFFFu, en = b.be[g] >> 16;
+                if (spans_more(st, en)) tail(t0 + g * RPW + grp, st, en);
             }
         };
         Batch A, B;
@@ -652,7 +684,7 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
     } else {
         // Two-stage pipeline over the wave's 64-tile batches: the run bounds of batch b+1 and the
         // data of batch b are in flight together, so each batch costs one memory latency, not two.
-        auto bounds = [&](uint32_t t0, uint32_t (&st)[8], uint32_t (&len)[8]) {
+        auto bounds = [&](uint32_t t0, uint32_t (&st)[8], uint32_t (&en)[8]) {
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
                 const uint32_t t = t0 + g * 8 + grp;  // the 8 lanes of a group read the same u16
@@ -662,39 +694,36 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
                     e = row_end[t];
                 }
                 st[g] = b;
-                len[g] = e - b;
+                en[g] = e;
             }
         };
-        uint32_t st[8], len[8];
-        bounds(tg, st, len);
+        uint32_t st[8], en[8];
+        bounds(tg, st, en);
         while (tg < t_hi) {
-            uint32_t nib[8];
+            uint32_t nib[8], ab[8];
             uint4 l[8];
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
-                if (q8 < len[g]) {
+                const uint32_t gi = (st[g] >> 3) + q8;
+                ab[g] = group_range(gi, st[g], en[g]);
+                if (ab[g]) {
                     const uint32_t* tile = tiles + (uint64_t)(tg + g * 8 + grp) * pl.tile_words;
-                    if (pl.ablate == 4) {  // timing experiment: synthetic indices, no tile loads
-                        l[g] = make_uint4(tg * 2654435761u + g, lane * 40503u, tg ^ lane, g * 977u);
-                        nib[g] = tg + lane;
-                    } else {
-                        load8(tile, pl.CP, st[g] + q8, l[g], nib[g]);
-                    }
+                    load_group(tile, gi, l[g], nib[g]);
                 }
             }
             const uint32_t tn = tg + step;
-            uint32_t st2[8], len2[8];
-            bounds(tn, st2, len2);
+            uint32_t st2[8], en2[8];
+            bounds(tn, st2, en2);
 #pragma unroll
             for (int g = 0; g < 8; ++g)
-                if (q8 < len[g]) or8(bitmap, l[g], nib[g], std::min<uint32_t>(8, len[g] - q8), pl.ablate);
+                if (ab[g]) or_group(bitmap, l[g], nib[g], ab[g] & 15u, ab[g] >> 4, abl);
 #pragma unroll
             for (int g = 0; g < 8; ++g)
-                if (len[g] > 64) tail(tg + g * 8 + grp, st[g], len[g]);
+                if (spans_more(st[g], en[g])) tail(tg + g * 8 + grp, st[g], en[g]);
 #pragma unroll
             for (int g = 0; g < 8; ++g) {
                 st[g] = st2[g];
-                len[g] = len2[g];
+                en[g] = en2[g];
             }
             tg = tn;
         }
@@ -730,21 +759,33 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
     // runtime k (the K = 0 kernel) keeps kStash / k rounds; compiled K values their own
     const bool ck = k == 4 || k == 9 || k == 10 || k == 19;
-    const uint32_t rmax = (uint32_t)(ck ? build_rounds_max((int)k, fixed) : rounds_max((int)k));
-    const uint32_t kpr = kPBlock / (uint32_t)(ck ? build_spl((int)k, fixed) : 1);  // keys per round
+    // K1 shape (k1_shape): the 512-thread one-lane-per-key workgroups where they exist (compiled
+    // k = 10 / 19, fixed-length keys, a scan of <= 4 * 512 segments), by default for k = 19 only
+    // (profiles/r03/matrix1.log, one box: k = 19 tile_sort 6.76 -> 6.24 ms; k = 10 even, 3.372 vs
+    // 3.374 ms).  VBF_K1 = 0 / 1 forces V = 0 / V = 1 where it exists.
+    static const int k1env = [] { const char* e = getenv("VBF_K1"); return e ? atoi(e) : -1; }();
     // packed u16 counters where they buy tile (VBF_C16 = 0 / 1 forces them off / on: A/B)
     static const int c16env = [] { const char* e = getenv("VBF_C16"); return e ? atoi(e) : -1; }();
     // measured (profiles/r03/ab_c16*.log): k = 10 +1 % (tiles of 3 020 -> 3 072 keys: full stash
     // rounds, fewer runs), k = 19 and k = 4 even (the extra VALU of the packed counters eats the
     // larger tiles' gain)
     pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) && (c16env >= 0 ? c16env != 0 : (k == 10 || k == 19)));
+    pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : k == 19) && fixed && (k == 10 || k == 19) && pl.c16 &&
+                        pl.nseg <= 4 * 512);
+    // K1 writes endsT[seg][tile] itself, no transpose pass (k = 19: -0.15 ms per 100M keys, k = 10
+    // -0.025 ms; VBF_ENDS_T = 0 keeps the transpose)
+    static const int etenv = [] { const char* e = getenv("VBF_ENDS_T"); return e ? atoi(e) : 1; }();
+    pl.ends_t = (uint32_t)(etenv != 0);
+    const K1Shape sh = k1_shape((int)k, fixed, (int)pl.k1v);
+    const uint32_t rmax = (uint32_t)(ck ? sh.rounds : rounds_max((int)k));
+    const uint32_t kpr = (uint32_t)sh.bs / (uint32_t)(ck ? sh.spl : 1);  // keys per round
     const uint32_t cnt_words = pl.c16 ? ((pl.nseg + 7) & ~7u) / 2 : pl.nseg_pad;
     pl.cnt_words = cnt_words;
     for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
         const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)cnt_words;
-        // LDS = 2.5 * CP with CP <= C + nseg + 8
-        const int64_t cmax = avail * 2 / 5 - pl.nseg - 8;
+        // LDS = 2.5 * CP with CP <= C + 7
+        const int64_t cmax = avail * 2 / 5 - 8;
         const int64_t kt = std::min<int64_t>((int64_t)rmax * kpr, cmax / k);
         if (kt >= kpr || per_cu == 1) {
             pl.KT = (uint32_t)std::max<int64_t>(kt, 1);
@@ -753,10 +794,10 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     }
     pl.R = (pl.KT + kpr - 1) / kpr;
     pl.C = pl.KT * k;
-    pl.CP = (pl.C + pl.nseg + 7) & ~7u;
-    pl.tile_words = pl.CP / 2 + pl.CP / 8;
+    pl.CP = (pl.C + 7) & ~7u;
+    pl.tile_words = (group_words(pl.CP) + 3) & ~3u;  // tiles start 16-byte aligned
     pl.nsegS = (pl.nseg + 7) & ~7u;
-    pl.lds1 = (pl.CP / 2 + pl.CP / 8 + cnt_words + 16 + kLenBuckets) * 4;
+    pl.lds1 = (group_words(pl.CP) + cnt_words + 16 + kLenBuckets) * 4;
     // VBF_TILE_LDS_MIN (experiments, speed only): request at least this much LDS per k_tile_pack
     // workgroup, e.g. > 80 KiB to hold one workgroup per CU
     static const int lds_min = [] { const char* e = getenv("VBF_TILE_LDS_MIN"); return e ? atoi(e) : 0; }();
@@ -778,8 +819,8 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     static const int lord = [] { const char* e = getenv("VBF_LEN_ORDER"); return e ? atoi(e) : 1; }();
     pl.len_order = (uint32_t)(lord != 0);
     static const int stg = [] { const char* e = getenv("VBF_STAGE_KEYS"); return e ? atoi(e) : 1; }();
-    // words: perm (KT u16) + begin + length (KT u32 each) inside the CP/2 words of low halves
-    pl.stage_keys = (uint32_t)(stg != 0 && (uint64_t)(pl.KT + 1) / 2 + 2ull * pl.KT <= pl.CP / 2);
+    // words: perm (KT u16) + begin + length (KT u32 each) inside the image's words
+    pl.stage_keys = (uint32_t)(stg != 0 && (uint64_t)(pl.KT + 1) / 2 + 2ull * pl.KT <= group_words(pl.CP));
     return pl;
 }
 
@@ -844,11 +885,16 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         else
             dk.keys = kb.keys + lo * kb.stride;
         const uint32_t ntiles = (uint32_t)((cn + pl.KT - 1) / pl.KT);
+        pl.ntS = (ntiles + 7) & ~7u;
         hipError_t err = hipSuccess;
         phase_begin(kPhaseTileSort, s);
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
             // m <= 2^31: the one-word remainder (fast_mod31); the runtime-k kernel keeps the general one
             auto pick = [&]<bool S>() {
+                if constexpr (FMT > 0 && S) {  // the 512-thread shape (make_plan: c16, m <= 2^31)
+                    if (pl.k1v && k == 10) return k_tile_pack<FMT, LP, 10, true, true, 1>;
+                    if (pl.k1v && k == 19) return k_tile_pack<FMT, LP, 19, true, true, 1>;
+                }
                 return k == 10 ? (pl.c16 ? k_tile_pack<FMT, LP, 10, S, true> : k_tile_pack<FMT, LP, 10, S>)
                      : k == 4  ? (pl.c16 ? k_tile_pack<FMT, LP, 4, S, true> : k_tile_pack<FMT, LP, 4, S>)
                      : k == 19 ? (pl.c16 ? k_tile_pack<FMT, LP, 19, S, true> : k_tile_pack<FMT, LP, 19, S>)
@@ -864,25 +910,30 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                 err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
             if (err == hipSuccess)
-                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
+                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles,
+                                   pl.ends_t ? endsT : ends);
         });
         if (err != hipSuccess) return err;
         phase_end(kPhaseTileSort, s);
-        phase_begin(kPhaseTranspose, s);
-        pl.ntS = (ntiles + 7) & ~7u;
-        err = launch_transpose_u16_strided(ends, endsT, ntiles, pl.nseg, pl.nsegS, pl.ntS, s);
-        if (err != hipSuccess) return err;
+        if (!pl.ends_t) {
+            phase_begin(kPhaseTranspose, s);
+            err = launch_transpose_u16_strided(ends, endsT, ntiles, pl.nseg, pl.nsegS, pl.ntS, s);
+            if (err != hipSuccess) return err;
+            phase_end(kPhaseTranspose, s);
+        }
         // several workgroups per segment when there are few segments (small m)
         pl.G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
         const bool merge = atomic_merge || pl.G > 1;
         // only the first chunk, and only where each segment has one sole writer, skips the read
         pl.fresh = (fresh && lo == 0 && !merge) ? 1u : 0u;
         if (fresh && lo == 0 && merge) return hipErrorInvalidValue;  // the caller zeroes first
-        phase_end(kPhaseTranspose, s);
         phase_begin(kPhaseSegOr, s);
-        // short runs (large k or m): the flattened variant; VBF_K3 overrides
-        const uint32_t k3v = pl.k3v ? pl.k3v : (pl.C / std::max(pl.nseg, 1u) < kShortRun ? 10u : 4u);
-        auto k3 = k3v == 10 ? k_seg_or<6, kPBlock, 4>
+        // the flattened variant, NG = 4 for short runs (large k or m), 5 otherwise (group layout,
+        // profiles/r03/matrix1.log: k = 10 seg_or 1.011 (V3) -> 0.861 ms, k = 19 NG 4 2.26 vs NG 5
+        // 2.34 ms); VBF_K3 overrides
+        const uint32_t k3v = pl.k3v ? pl.k3v : (pl.C / std::max(pl.nseg, 1u) < kShortRun ? 10u : 11u);
+        auto k3 = k3v == 13 ? k_seg_or<3, kPBlock, 4, 4>
+                : k3v == 10 ? k_seg_or<6, kPBlock, 4>
                 : k3v == 11 ? k_seg_or<6, kPBlock, 5>
                 : k3v == 12 ? k_seg_or<6, kPBlock, 6>
                 : k3v == 8 ? k_seg_or<3, kPBlock, 6>

@@ -47,6 +47,21 @@ __host__ __device__ constexpr int build_rounds_max(int k, bool fixed) {
     return build_spl(k, fixed) == 1 ? rounds_max(k) : kStash / build_kl(k, fixed);
 }
 
+// K1 workgroup shapes (k_tile_pack template parameter V).  V = 0: 1024 threads with the lanes per
+// key, seeds per lane and rounds above, at most 64 VGPRs (two workgroups per CU = 8 waves per SIMD).
+// V = 1 (compiled k = 10 / 19, fixed-length keys, <= 2048 segments): 512 threads, one lane per key,
+// up to 128 VGPRs -- two workgroups per CU are then 4 waves per SIMD, and the stash holds
+// kStashWide indices: k = 19 takes three rounds of 512 keys on one lane each (no idle 20th seed
+// slot, the prefix absorbed once), the same 1 536-key tile as V = 0.
+constexpr int kStashWide = 64;
+struct K1Shape {
+    int bs, spl, kl, rounds;
+};
+__host__ __device__ constexpr K1Shape k1_shape(int k, bool fixed, int v) {
+    if (v == 1) return K1Shape{512, 1, k, kStashWide / k < 6 ? kStashWide / k : 6};
+    return K1Shape{kPBlock, build_spl(k, fixed), build_kl(k, fixed), build_rounds_max(k, fixed)};
+}
+
 // Exclusive scan of v[0..n) in LDS (n <= 4 * kPBlock).  EVEN: scan the counts rounded up to even
 // (the build's even-length runs) in the same pass.  One barrier: after it every wave adds up the
 // totals of the waves before it itself instead of waiting for one wave to scan them.  The caller
