@@ -27,7 +27,7 @@ for s in $STEPS; do
     pytest) run pytest_gpu 1200 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;
     benchq)  run bench_quick 300 python bench.py --no-cpu-baseline ;;
-    bench19) run bench_k19 300 python bench.py --no-cpu-baseline --bits-per-key 19 --steps 10 ;;
+    bench19) run bench_k19 300 python bench.py --no-cpu-baseline --bits-per-key 19 --steps 100 ;;
     k19tests) run pytest_k19 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -v -m gpu -k "19 or config2" --timeout 600 --timeout-method thread ;;
     tile1wg) run bench_tile1wg 300 env VBF_TILE_LDS_MIN=98304 VBF_STAGGER=0 python bench.py --no-cpu-baseline --steps 10 ;;
     benchnostagger) run bench_nostagger 300 env VBF_STAGGER=0 python bench.py --no-cpu-baseline ;;

@@ -764,14 +764,16 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     // (profiles/r03/matrix1.log, one box: k = 19 tile_sort 6.76 -> 6.24 ms; k = 10 even, 3.372 vs
     // 3.374 ms).  VBF_K1 = 0 / 1 forces V = 0 / V = 1 where it exists.
     static const int k1env = [] { const char* e = getenv("VBF_K1"); return e ? atoi(e) : -1; }();
+    pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : k == 19) && fixed && (k == 10 || k == 19) && pl.nseg <= 4 * 512);
     // packed u16 counters where they buy tile (VBF_C16 = 0 / 1 forces them off / on: A/B)
     static const int c16env = [] { const char* e = getenv("VBF_C16"); return e ? atoi(e) : -1; }();
     // measured (profiles/r03/ab_c16*.log): k = 10 +1 % (tiles of 3 020 -> 3 072 keys: full stash
-    // rounds, fewer runs), k = 19 and k = 4 even (the extra VALU of the packed counters eats the
-    // larger tiles' gain)
-    pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) && (c16env >= 0 ? c16env != 0 : (k == 10 || k == 19)));
-    pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : k == 19) && fixed && (k == 10 || k == 19) && pl.c16 &&
-                        pl.nseg <= 4 * 512);
+    // rounds, fewer runs), k = 19 and k = 4 even with the 1024-thread K1 (the extra VALU of the
+    // packed counters eats the larger tiles' gain); the 512-thread k = 19 K1 holds its 1 536 keys
+    // with plain counters and is faster without the packing (tile_sort 6.18 -> 6.05 ms,
+    // profiles/r03/matrix3.log)
+    pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) &&
+                        (c16env >= 0 ? c16env != 0 : (k == 10 || (k == 19 && !pl.k1v))));
     // K1 writes endsT[seg][tile] itself, no transpose pass (k = 19: -0.15 ms per 100M keys, k = 10
     // -0.025 ms; VBF_ENDS_T = 0 keeps the transpose)
     static const int etenv = [] { const char* e = getenv("VBF_ENDS_T"); return e ? atoi(e) : 1; }();
@@ -891,9 +893,11 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
             // m <= 2^31: the one-word remainder (fast_mod31); the runtime-k kernel keeps the general one
             auto pick = [&]<bool S>() {
-                if constexpr (FMT > 0 && S) {  // the 512-thread shape (make_plan: c16, m <= 2^31)
-                    if (pl.k1v && k == 10) return k_tile_pack<FMT, LP, 10, true, true, 1>;
-                    if (pl.k1v && k == 19) return k_tile_pack<FMT, LP, 19, true, true, 1>;
+                if constexpr (FMT > 0 && S) {  // the 512-thread shape (make_plan: m <= 2^31)
+                    if (pl.k1v && k == 10) return pl.c16 ? k_tile_pack<FMT, LP, 10, true, true, 1>
+                                                         : k_tile_pack<FMT, LP, 10, true, false, 1>;
+                    if (pl.k1v && k == 19) return pl.c16 ? k_tile_pack<FMT, LP, 19, true, true, 1>
+                                                         : k_tile_pack<FMT, LP, 19, true, false, 1>;
                 }
                 return k == 10 ? (pl.c16 ? k_tile_pack<FMT, LP, 10, S, true> : k_tile_pack<FMT, LP, 10, S>)
                      : k == 4  ? (pl.c16 ? k_tile_pack<FMT, LP, 4, S, true> : k_tile_pack<FMT, LP, 4, S>)
