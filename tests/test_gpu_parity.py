@@ -486,25 +486,27 @@ def test_partitioned_build_knobs_same_words(vbf, ora, tmp_path):
             want[(m, k)] = np.unique((ora.hashes(b, k) % np.uint64(m)).ravel())
         else:
             want[(m, k)] = ora.build_words(b, m, k, threads=8)
-    combos = (("0", "0", "0"), ("1", "1", "0"), ("1", "0", "3"), ("0", "1", "1"), ("1", "1", "4"),
-              ("-1", "1", "12"), ("0", "0", "10"))
-    for k1, et, k3 in combos:
+    # (VBF_K1, VBF_ENDS_T, VBF_K3, VBF_K3_SPLIT): the last one splits k_seg_or's last round of
+    # segments over several workgroups (m = 2_999_999_999: 2 862 segments)
+    combos = (("0", "0", "0", "1"), ("1", "1", "0", "0"), ("1", "0", "3", "1"), ("0", "1", "1", "1"),
+              ("1", "1", "4", "1"), ("-1", "1", "12", "0"), ("0", "0", "10", "1"))
+    for k1, et, k3, sp in combos:
         env = {kk: vv for kk, vv in os.environ.items() if kk != "VBF_LIB"}
-        env["VBF_K1"], env["VBF_ENDS_T"], env["VBF_K3"] = k1, et, k3
-        stem = str(tmp_path / ("w%s%s%s" % (k1, et, k3)))
+        env["VBF_K1"], env["VBF_ENDS_T"], env["VBF_K3"], env["VBF_K3_SPLIT"] = k1, et, k3, sp
+        stem = str(tmp_path / ("w%s%s%s%s" % (k1, et, k3, sp)))
         r = subprocess.run([sys.executable, "-c", code, stem, str(tmp_path / "rows.npy")], env=env,
                            capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0 and "ok" in r.stdout, (k1, et, k3, r.stderr[-2000:])
+        assert r.returncode == 0 and "ok" in r.stdout, (k1, et, k3, sp, r.stderr[-2000:])
         for m, k in cases:
             nz, val = np.load(stem + "_%d_%d.npy" % (m, k))  # the child's nonzero words
             if m > 100_000_000:
                 bits = np.unpackbits(val.astype(np.uint32).view(np.uint8), bitorder="little").reshape(-1, 32)
                 idx = np.sort((nz[:, None] * np.uint64(32) + np.arange(32, dtype=np.uint64))[bits.astype(bool)])
-                assert np.array_equal(idx, want[(m, k)]), (k1, et, k3, m, k)
+                assert np.array_equal(idx, want[(m, k)]), (k1, et, k3, sp, m, k)
             else:
                 got = np.zeros((m + 31) // 32, np.uint32)
                 got[nz.astype(np.int64)] = val.astype(np.uint32)
-                assert np.array_equal(got, want[(m, k)]), (k1, et, k3, m, k)
+                assert np.array_equal(got, want[(m, k)]), (k1, et, k3, sp, m, k)
 
 
 @pytest.mark.parametrize("strategy", [1, 2])

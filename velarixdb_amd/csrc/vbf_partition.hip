@@ -49,6 +49,8 @@ struct PartPlan {
     uint32_t cnt_words;   // K1's counter words (a multiple of 4: the image stays 16-byte aligned)
     uint32_t k1v;         // K1's workgroup shape (k1_shape; VBF_K1)
     uint32_t ends_t;      // K1 writes the run ends transposed, endsT[seg][tile] (VBF_ENDS_T)
+    uint32_t nfull;       // K3: segments [0, nfull) one workgroup each; the rest split in P parts
+    uint32_t P;
     uint64_t m, mu, nwords;
 };
 
@@ -476,13 +478,26 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
     // XCD-aware order (blocks are dealt round-robin over the 8 XCDs; speed only, never
     // correctness): consecutive segments run on one XCD at the same time, and since a tile
     // stores its segments' runs back to back, they share the L2 lines those short runs sit in.
-    const uint32_t nwg = gridDim.x, q = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
-    const uint32_t wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + blockIdx.x / 8;
-    const uint32_t seg = wg / pl.G, part = wg % pl.G;
+    // Blocks [0, nfull): whole segments.  The rest: the last segments split into P parts (tile
+    // ranges) each, merged with word atomics -- the tail of the launch, dispatched last over all
+    // XCDs, so the last round of segments does not run on a few CUs while the others idle (k = 19:
+    // 1 812 segments = 7 rounds of 256 CUs + 20; launch_build_partitioned).
+    uint32_t seg, part, parts;
+    if (blockIdx.x < pl.nfull) {
+        const uint32_t nwg = pl.nfull, q = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+        seg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + blockIdx.x / 8;
+        part = 0;
+        parts = 1;
+    } else {
+        const uint32_t r = blockIdx.x - pl.nfull;
+        seg = pl.nfull + r / pl.P;
+        part = r % pl.P;
+        parts = pl.P;
+    }
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t wbase = (uint64_t)seg * kSegWords;
     const uint32_t wn = (uint32_t)std::min<uint64_t>(kSegWords, pl.nwords - wbase);
-    const bool own = (pl.G == 1) && !atomic_merge;  // sole writer: start from the existing words
+    const bool own = parts == 1 && !atomic_merge;  // sole writer: start from the existing words
     for (uint32_t w = tid * 4; w < kSegWords; w += BS * 4) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (own && !pl.fresh && pl.ablate < 6) {
@@ -498,8 +513,8 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
     }
     __syncthreads();
 
-    const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / pl.G);
-    const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / pl.G);
+    const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / parts);
+    const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / parts);
     const uint16_t* row_end = endsT + (uint64_t)seg * pl.ntS;
     const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * pl.ntS : nullptr;
     // V 0 / 3: LPR-lane groups, one run each (RPW runs per wave per load instruction)
@@ -865,6 +880,24 @@ bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k) {
     return true;
 }
 
+// Compute units of the current device (cached per device): K3's last-round split.
+static uint32_t cu_count() {
+    static uint32_t cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 0;
+        cache[dev] = (uint32_t)n;
+    }
+    return cache[dev];
+}
+// VBF_K3_SPLIT = 0 turns the split off (A/B; speed only)
+static bool tail_split_enabled() {
+    static const int v = [] { const char* e = getenv("VBF_K3_SPLIT"); return e ? atoi(e) : 1; }();
+    return v != 0;
+}
+
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
                                     void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s, bool fresh) {
     if (kb.n == 0 || k == 0) return hipSuccess;
@@ -931,6 +964,22 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         // only the first chunk, and only where each segment has one sole writer, skips the read
         pl.fresh = (fresh && lo == 0 && !merge) ? 1u : 0u;
         if (fresh && lo == 0 && merge) return hipErrorInvalidValue;  // the caller zeroes first
+        // K3 runs one workgroup per CU (128 KiB of LDS); when the segments leave a last round of
+        // few workgroups (nseg % CUs small), those segments are split over several workgroups each
+        pl.nfull = pl.G > 1 ? 0u : pl.nseg;
+        pl.P = pl.G;
+        if (pl.G == 1 && tail_split_enabled()) {
+            const uint32_t ncu = cu_count(), rem = ncu ? pl.nseg % ncu : 0u;
+            if (pl.nseg > ncu && rem > 0 && ncu / rem >= 2) {
+                pl.P = std::min<uint32_t>(std::min<uint32_t>(ncu / rem, 16u), ntiles);
+                pl.nfull = pl.nseg - rem;
+            }
+        }
+        if (pl.fresh && pl.nfull < pl.nseg) {  // the split segments' words: zero, then ORed into
+            const uint64_t w0 = (uint64_t)pl.nfull * kSegWords;
+            err = hipMemsetAsync(words + w0, 0, (pl.nwords - w0) * 4, s);
+            if (err != hipSuccess) return err;
+        }
         phase_begin(kPhaseSegOr, s);
         // the flattened variant, NG = 4 for short runs (large k or m), 5 otherwise (group layout,
         // profiles/r03/matrix1.log: k = 10 seg_or 1.011 (V3) -> 0.861 ms, k = 19 NG 4 2.26 vs NG 5
@@ -947,7 +996,8 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                 : k3v == 1 ? k_seg_or<0>
                            : k_seg_or<3, kPBlock, 5>;
         const int bs = (k3v == 5 || k3v == 6) ? 768 : kPBlock;
-        hipLaunchKernelGGL(k3, dim3(pl.nseg * pl.G), dim3(bs), 0, s, tiles, endsT, ntiles, pl, merge, words);
+        hipLaunchKernelGGL(k3, dim3(pl.nfull + (pl.nseg - pl.nfull) * pl.P), dim3(bs), 0, s, tiles, endsT, ntiles,
+                           pl, merge, words);
         phase_end(kPhaseSegOr, s);
         err = hipGetLastError();
         if (err != hipSuccess) return err;
