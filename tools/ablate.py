@@ -5,7 +5,7 @@ Needs the ablation build of the library (the product libvbf.so ignores VBF_ABLAT
 `python velarixdb_amd/build.py --ablation` writes velarixdb_amd/libvbf_ablate.so, which the
 children load through VBF_LIB.
 
-Runs the config-2 build in child processes with VBF_ABLATE=0/1/2 and prints the library's
+Runs the config-2 build (ABL_M / ABL_K override m and k, e.g. 1900000000 / 19) in child processes with VBF_ABLATE=0/1/2 and prints the library's
 per-phase hipEvent timings: 0 = full build, 1 = hash + count + scan (no place/copy),
 2 = hash only (no LDS count either), 3 = seg_or loads without ds_or, 4 = seg_or ds_or on
 synthetic indices without tile loads,
@@ -21,7 +21,8 @@ import ctypes, json, os, sys, torch
 sys.path.insert(0, os.environ["ROOT"])
 import velarixdb_amd as vbf
 from velarixdb_amd._lib import call, lib, profile_read
-n, L, m, k = 100_000_000, 16, 1_000_000_000, 10
+n, L = 100_000_000, 16
+m, k = int(os.environ.get("ABL_M", "1000000000")), int(os.environ.get("ABL_K", "10"))
 dev = torch.device("cuda:0")
 sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 keys = torch.empty(n * L, dtype=torch.uint8, device=dev)

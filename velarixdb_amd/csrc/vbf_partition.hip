@@ -775,20 +775,22 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     // runtime k (the K = 0 kernel) keeps kStash / k rounds; compiled K values their own
     const bool ck = k == 4 || k == 9 || k == 10 || k == 19;
     // K1 shape (k1_shape): the 512-thread one-lane-per-key workgroups where they exist (compiled
-    // k = 10 / 19, fixed-length keys, a scan of <= 4 * 512 segments), by default for k = 19 only
-    // (profiles/r03/matrix1.log, one box: k = 19 tile_sort 6.76 -> 6.24 ms; k = 10 even, 3.372 vs
-    // 3.374 ms).  VBF_K1 = 0 / 1 forces V = 0 / V = 1 where it exists.
+    // k = 10 / 19, fixed-length keys, a scan of <= 4 * 512 segments), by default (profiles/r03/
+    // matrix1.log, one box: k = 19 tile_sort 6.76 -> 6.24 ms; k = 10 even with packed counters,
+    // and with plain ones 3.36 -> 3.28 ms, matrix7.log).  VBF_K1 = 0 / 1 forces V = 0 / V = 1
+    // where it exists.
     static const int k1env = [] { const char* e = getenv("VBF_K1"); return e ? atoi(e) : -1; }();
-    pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : k == 19) && fixed && (k == 10 || k == 19) && pl.nseg <= 4 * 512);
+    pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : true) && fixed && (k == 10 || k == 19) && pl.nseg <= 4 * 512);
     // packed u16 counters where they buy tile (VBF_C16 = 0 / 1 forces them off / on: A/B)
     static const int c16env = [] { const char* e = getenv("VBF_C16"); return e ? atoi(e) : -1; }();
-    // measured (profiles/r03/ab_c16*.log): k = 10 +1 % (tiles of 3 020 -> 3 072 keys: full stash
-    // rounds, fewer runs), k = 19 and k = 4 even with the 1024-thread K1 (the extra VALU of the
-    // packed counters eats the larger tiles' gain); the 512-thread k = 19 K1 holds its 1 536 keys
-    // with plain counters and is faster without the packing (tile_sort 6.18 -> 6.05 ms,
-    // profiles/r03/matrix3.log)
+    // measured: with the split image (runs padded, CP = C + nseg) they bought k = 10 its full
+    // third stash round (3 020 -> 3 072 keys, +1 %, profiles/r03/ab_c16.log); the group image
+    // needs no run padding and holds 3 072 keys with plain counters, which then skip the packing's
+    // VALU (k = 10 tile_sort 3.37 -> 3.26 ms, profiles/r03/matrix5.log; the 512-thread k = 19 K1
+    // likewise 6.18 -> 6.05 ms, matrix3.log).  Only the 1 024-thread k = 19 shape (two lanes per
+    // key: m > 2^31) keeps them, for its 1 536-key tile.
     pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) &&
-                        (c16env >= 0 ? c16env != 0 : (k == 10 || (k == 19 && !pl.k1v))));
+                        (c16env >= 0 ? c16env != 0 : (k == 19 && !pl.k1v)));
     // K1 writes endsT[seg][tile] itself, no transpose pass (k = 19: -0.15 ms per 100M keys, k = 10
     // -0.025 ms; VBF_ENDS_T = 0 keeps the transpose)
     static const int etenv = [] { const char* e = getenv("VBF_ENDS_T"); return e ? atoi(e) : 1; }();
@@ -813,6 +815,12 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     pl.C = pl.KT * k;
     pl.CP = (pl.C + 7) & ~7u;
     pl.tile_words = (group_words(pl.CP) + 3) & ~3u;  // tiles start 16-byte aligned
+    // VBF_TILE_PAD (speed only; default 4 words): extra words per tile in the workspace, which
+    // move the tile stride off large powers of two -- k_seg_or reads the runs of consecutive tiles
+    // at the same offset in each, and k = 10's 76 800-byte stride is a multiple of 1 KiB (seg_or
+    // 0.848 -> 0.829 ms with 16 bytes of pad, k = 19 even; profiles/r03/matrix6.log)
+    static const int tpad = [] { const char* e = getenv("VBF_TILE_PAD"); return e ? atoi(e) : 4; }();
+    pl.tile_words += (uint32_t)std::max(0, tpad) & ~3u;
     pl.nsegS = (pl.nseg + 7) & ~7u;
     pl.lds1 = (group_words(pl.CP) + cnt_words + 16 + kLenBuckets) * 4;
     // VBF_TILE_LDS_MIN (experiments, speed only): request at least this much LDS per k_tile_pack
