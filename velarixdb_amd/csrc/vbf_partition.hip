@@ -63,6 +63,7 @@ constexpr int kLenBuckets = 32;
 
 // With sbeg/slen (not null) the second pass also stages each key's (begin - base, length) at its
 // sorted slot, so the hashing rounds read them from LDS instead of a dependent offsets load.
+template <int BS = kPBlock>
 __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, uint32_t nk, uint16_t* perm,
                                              uint32_t* hist, uint32_t* sbeg = nullptr, uint32_t* slen = nullptr,
                                              uint64_t base = 0) {
@@ -71,7 +72,7 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
         const uint64_t len = dk.offsets[key0 + l + 1] - dk.offsets[key0 + l];
         return (uint32_t)std::min<uint64_t>(len >> 3, kLenBuckets - 1);
     };
-    for (uint32_t l = tid; l < nk; l += kPBlock) atomicAdd(&hist[bucket(l)], 1u);
+    for (uint32_t l = tid; l < nk; l += BS) atomicAdd(&hist[bucket(l)], 1u);
     __syncthreads();
     if (tid < 64) {
         const uint32_t v = tid < kLenBuckets ? hist[tid] : 0u;
@@ -84,7 +85,7 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
         if (tid < kLenBuckets) hist[tid] = incl - v;
     }
     __syncthreads();
-    for (uint32_t l = tid; l < nk; l += kPBlock) {
+    for (uint32_t l = tid; l < nk; l += BS) {
         const uint64_t b = dk.offsets[key0 + l], len = dk.offsets[key0 + l + 1] - b;
         const uint32_t pos = atomicAdd(&hist[(uint32_t)std::min<uint64_t>(len >> 3, kLenBuckets - 1)], 1u);
         perm[pos] = (uint16_t)l;
@@ -151,7 +152,7 @@ template <int FMT, bool LP, int K, bool M31, bool C16 = false, int V = 0>
 __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile_pack(DevKeys dk, PartPlan pl,
                                                                                       uint32_t* tiles, uint16_t* ends) {
     constexpr int BS = V == 1 ? 512 : kPBlock;  // k1_shape(K, FMT > 0, V).bs
-    static_assert(V == 0 || (K > 0 && FMT > 0), "the 512-thread shape is for compiled k and fixed-length keys");
+    static_assert(V == 0 || K > 0, "the 512-thread shape is for compiled k");
     extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
     // The per-segment counters first, at LDS address 0 (the kernel has no static LDS, so the
     // dynamic allocation starts there; launch_build_partitioned checks it): the count and rank
@@ -208,9 +209,9 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
                 staged = dk.offsets[key_end] - sbase < (1ull << 32);
             }
             if (staged)
-                length_order(dk, key0, nk, lo, lhist, smem + sw0, smem + sw0 + nk, sbase);
+                length_order<BS>(dk, key0, nk, lo, lhist, smem + sw0, smem + sw0 + nk, sbase);
             else
-                length_order(dk, key0, nk, lo, lhist);
+                length_order<BS>(dk, key0, nk, lo, lhist);
         }
     }
     auto key_of = [&](uint32_t slot) -> uint64_t { return key0 + (perm ? (uint32_t)lo[slot] : slot); };
@@ -775,29 +776,29 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     // runtime k (the K = 0 kernel) keeps kStash / k rounds; compiled K values their own
     const bool ck = k == 4 || k == 9 || k == 10 || k == 19;
     // K1 shape (k1_shape): the 512-thread one-lane-per-key workgroups where they exist (compiled
-    // k = 10 / 19, fixed-length keys, a scan of <= 4 * 512 segments), by default (profiles/r03/
-    // matrix1.log, one box: k = 19 tile_sort 6.76 -> 6.24 ms; k = 10 even with packed counters,
-    // and with plain ones 3.36 -> 3.28 ms, matrix7.log).  VBF_K1 = 0 / 1 forces V = 0 / V = 1
-    // where it exists.
+    // k = 10 / 19, a scan of <= 4 * 512 segments), by default (profiles/r03/matrix1.log, one box:
+    // k = 19 tile_sort 6.76 -> 6.24 ms; k = 10 even with packed counters, and with plain ones
+    // 3.36 -> 3.28 ms, matrix7.log).  Runtime-length layouts take it with plain counters only.
+    // VBF_K1 = 0 / 1 forces V = 0 / V = 1 where it exists.
     static const int k1env = [] { const char* e = getenv("VBF_K1"); return e ? atoi(e) : -1; }();
-    pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : true) && fixed && (k == 10 || k == 19) && pl.nseg <= 4 * 512);
+    pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : true) && (k == 10 || k == 19) && pl.nseg <= 4 * 512);
     // packed u16 counters where they buy tile (VBF_C16 = 0 / 1 forces them off / on: A/B)
     static const int c16env = [] { const char* e = getenv("VBF_C16"); return e ? atoi(e) : -1; }();
     // measured: with the split image (runs padded, CP = C + nseg) they bought k = 10 its full
     // third stash round (3 020 -> 3 072 keys, +1 %, profiles/r03/ab_c16.log); the group image
     // needs no run padding and holds 3 072 keys with plain counters, which then skip the packing's
-    // VALU (k = 10 tile_sort 3.37 -> 3.26 ms, profiles/r03/matrix5.log; the 512-thread k = 19 K1
-    // likewise 6.18 -> 6.05 ms, matrix3.log).  Only the 1 024-thread k = 19 shape (two lanes per
-    // key: m > 2^31) keeps them, for its 1 536-key tile.
+    // VALU (the 512-thread k = 19 K1: 6.18 -> 6.05 ms, matrix3.log; k = 10 even).  Only the
+    // 1 024-thread k = 19 shape (two lanes per key: m > 2^31) keeps them, for its 1 536-key tile.
     pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) &&
                         (c16env >= 0 ? c16env != 0 : (k == 19 && !pl.k1v)));
+    if (!fixed && pl.c16) pl.k1v = 0;
+    const K1Shape sh = k1_shape((int)k, fixed, (int)pl.k1v);
+    const uint32_t rmax = (uint32_t)(ck ? sh.rounds : rounds_max((int)k));
+    const uint32_t kpr = (uint32_t)sh.bs / (uint32_t)(ck ? sh.spl : 1);  // keys per round
     // K1 writes endsT[seg][tile] itself, no transpose pass (k = 19: -0.15 ms per 100M keys, k = 10
     // -0.025 ms; VBF_ENDS_T = 0 keeps the transpose)
     static const int etenv = [] { const char* e = getenv("VBF_ENDS_T"); return e ? atoi(e) : 1; }();
     pl.ends_t = (uint32_t)(etenv != 0);
-    const K1Shape sh = k1_shape((int)k, fixed, (int)pl.k1v);
-    const uint32_t rmax = (uint32_t)(ck ? sh.rounds : rounds_max((int)k));
-    const uint32_t kpr = (uint32_t)sh.bs / (uint32_t)(ck ? sh.spl : 1);  // keys per round
     const uint32_t cnt_words = pl.c16 ? ((pl.nseg + 7) & ~7u) / 2 : pl.nseg_pad;
     pl.cnt_words = cnt_words;
     for (uint32_t per_cu : {2u, 1u}) {
@@ -939,6 +940,9 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                                                          : k_tile_pack<FMT, LP, 10, true, false, 1>;
                     if (pl.k1v && k == 19) return pl.c16 ? k_tile_pack<FMT, LP, 19, true, true, 1>
                                                          : k_tile_pack<FMT, LP, 19, true, false, 1>;
+                } else if constexpr (S) {  // runtime-length layouts: plain counters only (make_plan)
+                    if (pl.k1v && k == 10) return k_tile_pack<FMT, LP, 10, true, false, 1>;
+                    if (pl.k1v && k == 19) return k_tile_pack<FMT, LP, 19, true, false, 1>;
                 }
                 return k == 10 ? (pl.c16 ? k_tile_pack<FMT, LP, 10, S, true> : k_tile_pack<FMT, LP, 10, S>)
                      : k == 4  ? (pl.c16 ? k_tile_pack<FMT, LP, 4, S, true> : k_tile_pack<FMT, LP, 4, S>)
