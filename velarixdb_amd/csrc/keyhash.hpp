@@ -74,51 +74,75 @@ __device__ __forceinline__ Prefix absorb_fixed(const FixedWords<FMT>& kw) {
     return p;
 }
 
+// A runtime-length key's first five source words (the absorb's first four blocks and the
+// shifted-in fifth), loaded apart from the absorb so a caller can issue the next key's loads
+// before hashing this one (k_tile_pack's offsets layout: one round of keys ahead).
+struct KeyHead {
+    const uint64_t* wbase;
+    uintptr_t wstart, end;
+    uint64_t len;
+    uint32_t sh;
+    uint64_t w[5];
+};
+
+__device__ __forceinline__ KeyHead key_head_load(const uint8_t* keys, uint64_t beg, uint64_t len) {
+    KeyHead h;
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(keys + beg);
+    h.end = addr + len;
+    h.wstart = addr & ~(uintptr_t)7;
+    h.wbase = reinterpret_cast<const uint64_t*>(h.wstart);
+    h.sh = (uint32_t)(addr & 7) * 8;
+    h.len = len;
+    h.w[0] = len ? ld_word(h.wbase, h.wstart, h.end, 0) : 0ull;
+#pragma unroll
+    for (int i = 1; i < 5; ++i) h.w[i] = ld_word(h.wbase, h.wstart, h.end, i);
+    return h;
+}
+
+// The runtime-length absorb from a loaded head.
+template <bool LP>
+__device__ __forceinline__ Prefix key_prefix_head(const KeyHead& h) {
+    Prefix p;
+    const uint64_t len = h.len;
+    const uint32_t sh = h.sh;
+    Sip st = sip_init();
+    if constexpr (LP) sip_compress(st, len);
+    const uint64_t nfull = len >> 3;
+    // Source words c+1..c+4 sit in a[] while words c+5..c+8 are already in flight in b[]:
+    // the absorb never waits on a load it just issued (a word past the key reads as 0).
+    uint64_t lo = h.w[0];
+    uint64_t a[4] = {h.w[1], h.w[2], h.w[3], h.w[4]};
+    uint64_t c = 0;
+    for (; c + 4 <= nfull; c += 4) {
+        uint64_t b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b[i] = ld_word(h.wbase, h.wstart, h.end, c + 5 + i);
+        sip_compress(st, funnel(lo, a[0], sh));
+        sip_compress(st, funnel(a[0], a[1], sh));
+        sip_compress(st, funnel(a[1], a[2], sh));
+        sip_compress(st, funnel(a[2], a[3], sh));
+        lo = a[3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = b[i];
+    }
+    // 0..3 full blocks left: words c+1.. are a[0..]; the tail's upper word is a[nfull - c]
+    const uint32_t left = (uint32_t)(nfull - c);
+    uint64_t up = a[0];
+    if (left > 0) { sip_compress(st, funnel(lo, a[0], sh)); lo = a[0]; up = a[1]; }
+    if (left > 1) { sip_compress(st, funnel(lo, a[1], sh)); lo = a[1]; up = a[2]; }
+    if (left > 2) { sip_compress(st, funnel(lo, a[2], sh)); lo = a[2]; up = a[3]; }
+    p.st = st;
+    p.r = (uint32_t)(len & 7);  // P % 8 == len % 8 (the length block is 8 bytes)
+    const uint64_t tmask = p.r ? (~0ull >> (64 - 8 * p.r)) : 0ull;
+    p.tail = p.r ? (funnel(lo, up, sh) & tmask) : 0ull;
+    p.total = (uint32_t)((len + (LP ? 8 : 0) + 8) & 0xff);
+    return p;
+}
+
 // Any key given as (byte position in `keys`, length): the runtime-length absorb.
 template <bool LP>
 __device__ __forceinline__ Prefix key_prefix_at(const uint8_t* keys, uint64_t beg, uint64_t len) {
-    Prefix p;
-    {
-        const uintptr_t addr = reinterpret_cast<uintptr_t>(keys + beg);
-        const uintptr_t end = addr + len;
-        const uintptr_t wstart = addr & ~(uintptr_t)7;
-        const uint64_t* wbase = reinterpret_cast<const uint64_t*>(wstart);
-        const uint32_t sh = (uint32_t)(addr & 7) * 8;
-        Sip st = sip_init();
-        if constexpr (LP) sip_compress(st, len);
-        const uint64_t nfull = len >> 3;
-        // Source words c+1..c+4 sit in a[] while words c+5..c+8 are already in flight in b[]:
-        // the absorb never waits on a load it just issued (a word past the key reads as 0).
-        uint64_t lo = len ? ld_word(wbase, wstart, end, 0) : 0ull;
-        uint64_t a[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = ld_word(wbase, wstart, end, 1 + i);
-        uint64_t c = 0;
-        for (; c + 4 <= nfull; c += 4) {
-            uint64_t b[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) b[i] = ld_word(wbase, wstart, end, c + 5 + i);
-            sip_compress(st, funnel(lo, a[0], sh));
-            sip_compress(st, funnel(a[0], a[1], sh));
-            sip_compress(st, funnel(a[1], a[2], sh));
-            sip_compress(st, funnel(a[2], a[3], sh));
-            lo = a[3];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = b[i];
-        }
-        // 0..3 full blocks left: words c+1.. are a[0..]; the tail's upper word is a[nfull - c]
-        const uint32_t left = (uint32_t)(nfull - c);
-        uint64_t up = a[0];
-        if (left > 0) { sip_compress(st, funnel(lo, a[0], sh)); lo = a[0]; up = a[1]; }
-        if (left > 1) { sip_compress(st, funnel(lo, a[1], sh)); lo = a[1]; up = a[2]; }
-        if (left > 2) { sip_compress(st, funnel(lo, a[2], sh)); lo = a[2]; up = a[3]; }
-        p.st = st;
-        p.r = (uint32_t)(len & 7);  // P % 8 == len % 8 (the length block is 8 bytes)
-        const uint64_t tmask = p.r ? (~0ull >> (64 - 8 * p.r)) : 0ull;
-        p.tail = p.r ? (funnel(lo, up, sh) & tmask) : 0ull;
-        p.total = (uint32_t)((len + (LP ? 8 : 0) + 8) & 0xff);
-    }
-    return p;
+    return key_prefix_head<LP>(key_head_load(keys, beg, len));
 }
 
 template <int FMT, bool LP>

@@ -222,23 +222,47 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
         // static even where the round body holds a runtime loop (the offsets layout's absorb),
         // which keeps LLVM from unrolling a plain `for` -- the stash then went to scratch
         // memory (128 B per lane of scratch stores and loads per key, variable-length builds).
+        // Runtime-length layouts on the 512-thread shape (128 VGPRs): the first five source words
+        // of a lane's next-round key are loaded before this round's absorb, so they arrive while
+        // this round hashes (config 3: the absorb waited on its first loads).
+        constexpr bool PF = FMT <= 0 && V == 1;
+        auto key_span = [&](uint32_t slot, uint64_t& beg, uint64_t& len) {
+            if constexpr (FMT < 0) {
+                if (staged) {
+                    beg = sbase - dk.off_base + smem[sw0 + slot];
+                    len = smem[sw0 + nk + slot];
+                } else {
+                    const uint64_t j = key_of(slot);
+                    beg = dk.offsets[j] - dk.off_base;
+                    len = dk.offsets[j + 1] - dk.offsets[j];
+                }
+            } else {
+                beg = key_of(slot) * dk.stride;
+                len = dk.stride;
+            }
+        };
+        auto head_of = [&](uint32_t rr) -> KeyHead {
+            const uint32_t slot = rr * kKeysPerRound + tid / SPL;
+            uint64_t beg = 0, len = 0;  // no key: a zero-length head reads nothing
+            if (rr < pl.R && slot < nk) key_span(slot, beg, len);
+            return key_head_load(dk.keys, beg, len);
+        };
+        KeyHead head_cur{};
+        if constexpr (PF) head_cur = head_of(0);
         auto round = [&](auto rc) {
             constexpr int r = decltype(rc)::value;
             const uint32_t slot = (uint32_t)r * kKeysPerRound + tid / SPL;
             const uint32_t seed0 = (uint32_t)KL * (tid % SPL);
             const bool valid = (uint32_t)r < pl.R && slot < nk;
             Prefix p{};
-            if (valid) {
+            if constexpr (PF) {
+                const KeyHead h = head_cur;
+                if constexpr (r + 1 < RM) head_cur = head_of(r + 1);
+                if (valid) p = key_prefix_head<LP>(h);
+            } else if (valid) {
                 if constexpr (FMT < 0) {
                     uint64_t beg, len;
-                    if (staged) {
-                        beg = sbase - dk.off_base + smem[sw0 + slot];
-                        len = smem[sw0 + nk + slot];
-                    } else {
-                        const uint64_t j = key_of(slot);
-                        beg = dk.offsets[j] - dk.off_base;
-                        len = dk.offsets[j + 1] - dk.offsets[j];
-                    }
+                    key_span(slot, beg, len);
                     p = key_prefix_at<LP>(dk.keys, beg, len);
                 } else {
                     p = key_prefix<FMT, LP>(dk, key_of(slot));
