@@ -913,24 +913,6 @@ bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k) {
     return true;
 }
 
-// Compute units of the current device (cached per device): K3's last-round split.
-static uint32_t cu_count() {
-    static uint32_t cache[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (!cache[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 0;
-        cache[dev] = (uint32_t)n;
-    }
-    return cache[dev];
-}
-// VBF_K3_SPLIT = 0 turns the split off (A/B; speed only)
-static bool tail_split_enabled() {
-    static const int v = [] { const char* e = getenv("VBF_K3_SPLIT"); return e ? atoi(e) : 1; }();
-    return v != 0;
-}
-
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
                                     void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s, bool fresh) {
     if (kb.n == 0 || k == 0) return hipSuccess;
@@ -1005,7 +987,7 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         pl.nfull = pl.G > 1 ? 0u : pl.nseg;
         pl.P = pl.G;
         if (pl.G == 1 && tail_split_enabled()) {
-            const uint32_t ncu = cu_count(), rem = ncu ? pl.nseg % ncu : 0u;
+            const uint32_t ncu = device_cu_count(), rem = ncu ? pl.nseg % ncu : 0u;
             if (pl.nseg > ncu && rem > 0 && ncu / rem >= 2) {
                 pl.P = std::min<uint32_t>(std::min<uint32_t>(ncu / rem, 16u), ntiles);
                 pl.nfull = pl.nseg - rem;

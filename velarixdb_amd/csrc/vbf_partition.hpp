@@ -133,6 +133,26 @@ __device__ __forceinline__ void block_exclusive_scan16(uint32_t* v, uint32_t n, 
     if (tid * 2 + 1 < (n + 1) / 2) v[tid * 2 + 1] = r2 | (r3 << 16);
 }
 
+// Compute units of the current device, cached per device: the segment kernels run one workgroup
+// per CU (128 KiB of LDS) and split a short last round of segments over the idle ones.
+inline uint32_t device_cu_count() {
+    static uint32_t cache[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cache[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 0;
+        cache[dev] = (uint32_t)n;
+    }
+    return cache[dev];
+}
+// VBF_K3_SPLIT = 0 turns the last-round split of k_seg_or and k_probe_seg off (A/B; speed only)
+inline bool tail_split_enabled() {
+    static const int v = [] { const char* e = getenv("VBF_K3_SPLIT"); return e ? atoi(e) : 1; }();
+    return v != 0;
+}
+inline bool probe_split_enabled() { return tail_split_enabled(); }
+
 // K2 (vbf_partition.hip): ends[rows][cols] -> endsT[cols][rows], shared by build and probe.
 void launch_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows, uint32_t cols, hipStream_t s);
 // The same with row strides (in: in_stride, out: out_stride elements); both multiples of 8 and

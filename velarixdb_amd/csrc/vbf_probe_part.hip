@@ -123,14 +123,29 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
 //   1: the k_seg_or<3> scheme -- a wave serves 8 * NG tiles per batch, run bounds loaded
 //      coalesced and spread with ds_bpermute, bounds of b+2 / entries of b+1 / bit tests of b in
 //      flight together, unconditional entry loads (idle lanes re-read their run's start)
+// Blocks [0, nfull): whole segments, XCD-aware.  The rest: segments [nfull, nseg) split into P
+// tile ranges each (every segment when segments are few; otherwise the last, short round of
+// segment workgroups, spread over the idle CUs).  Results are per entry, so parts need no merge:
+// a split costs only the segment's filter words loaded once more per part.
 template <int V, int NG = 4>
 __global__ __launch_bounds__(kPBlock) void k_probe_seg(const uint32_t* tiles, const uint16_t* endsT, uint32_t ntiles,
-                                                       ProbePlan pl, uint32_t G, const uint32_t* words, uint8_t* res) {
+                                                       ProbePlan pl, uint32_t nfull, uint32_t P, const uint32_t* words,
+                                                       uint8_t* res) {
     __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
-    const uint32_t nwg = gridDim.x, qq = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
-    const uint32_t wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + blockIdx.x / 8;
-    const uint32_t seg = wg / G, part = wg % G;  // several workgroups per segment when segments are few
-    const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / G), t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / G);
+    uint32_t seg, part, parts;
+    if (blockIdx.x < nfull) {
+        const uint32_t qq = nfull / 8, r8 = nfull % 8, xcd = blockIdx.x % 8;
+        seg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + blockIdx.x / 8;
+        part = 0;
+        parts = 1;
+    } else {
+        const uint32_t r = blockIdx.x - nfull;
+        seg = nfull + r / P;
+        part = r % P;
+        parts = P;
+    }
+    const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / parts);
+    const uint32_t t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / parts);
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint64_t wbase = (uint64_t)seg * kSegWords;
     const uint32_t wn = (uint32_t)std::min<uint64_t>(kSegWords, pl.nwords - wbase);
@@ -398,10 +413,24 @@ hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         phase_end(kPhaseProbePack, s);
         phase_begin(kPhaseProbeSeg, s);
         const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
+        uint32_t nfull = G > 1 ? 0u : pl.nseg, P = G;
+        if (G == 1 && probe_split_enabled()) {
+            // the last round's rem segments in P parts: P minimising ceil(rem * P / CUs) / P, the
+            // rounds of part-workgroups the tail then takes (k = 19, m = 1.9e9: 1 812 = 7 x 256 +
+            // 20 -> P = 12; k = 10, m = 1e9: 954 = 3 x 256 + 186 -> P = 11)
+            const uint32_t ncu = device_cu_count(), rem = ncu ? pl.nseg % ncu : 0u;
+            if (pl.nseg > ncu && rem > 0) {
+                double best = 1.0;
+                for (uint32_t p = 2; p <= 16 && p <= ntiles; ++p) {
+                    const double t = (double)((rem * p + ncu - 1) / ncu) / p;
+                    if (t < best - 1e-9) { best = t; P = p; }
+                }
+                if (P > 1) nfull = pl.nseg - rem;
+            }
+        }
         static const int q3v = [] { const char* e = getenv("VBF_Q3"); return e ? atoi(e) : 1; }();
-        hipLaunchKernelGGL(q3v == 1 ? k_probe_seg<1> : k_probe_seg<0>, dim3(pl.nseg * G), dim3(kPBlock), 0, s, tiles,
-                           endsT, ntiles, pl, G, words,
-                           res);
+        hipLaunchKernelGGL(q3v == 1 ? k_probe_seg<1> : k_probe_seg<0>, dim3(nfull + (pl.nseg - nfull) * P),
+                           dim3(kPBlock), 0, s, tiles, endsT, ntiles, pl, nfull, P, words, res);
         phase_end(kPhaseProbeSeg, s);
         phase_begin(kPhaseProbeOut, s);
         if (count) {
