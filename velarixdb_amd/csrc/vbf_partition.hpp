@@ -49,7 +49,8 @@ __host__ __device__ constexpr int build_rounds_max(int k, bool fixed) {
 
 // K1 workgroup shapes (k_tile_pack template parameter V).  V = 0: 1024 threads with the lanes per
 // key, seeds per lane and rounds above, at most 64 VGPRs (two workgroups per CU = 8 waves per SIMD).
-// V = 1 (compiled k = 10 / 19, fixed-length keys, <= 2048 segments): 512 threads, one lane per key,
+// V = 1 (compiled k = 10 / 19, <= 2048 segments; runtime-length layouts with plain counters): 512
+// threads, one lane per key,
 // up to 128 VGPRs -- two workgroups per CU are then 4 waves per SIMD, and the stash holds
 // kStashWide indices: k = 19 takes three rounds of 512 keys on one lane each (no idle 20th seed
 // slot, the prefix absorbed once), the same 1 536-key tile as V = 0.
