@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <utility>
 
@@ -137,15 +138,17 @@ __device__ __forceinline__ void block_exclusive_scan16(uint32_t* v, uint32_t n, 
 // Compute units of the current device, cached per device: the segment kernels run one workgroup
 // per CU (128 KiB of LDS) and split a short last round of segments over the idle ones.
 inline uint32_t device_cu_count() {
-    static uint32_t cache[64] = {};
+    static std::atomic<uint32_t> cache[64] = {};  // builds run from several host threads
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (!cache[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 0;
-        cache[dev] = (uint32_t)n;
+    uint32_t n = cache[dev].load(std::memory_order_relaxed);
+    if (!n) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 0;
+        n = (uint32_t)v;
+        cache[dev].store(n, std::memory_order_relaxed);
     }
-    return cache[dev];
+    return n;
 }
 // VBF_K3_SPLIT = 0 turns the last-round split of k_seg_or and k_probe_seg off (A/B; speed only)
 inline bool tail_split_enabled() {
