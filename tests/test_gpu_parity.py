@@ -489,7 +489,7 @@ def test_partitioned_build_knobs_same_words(vbf, ora, tmp_path):
     # (VBF_K1, VBF_ENDS_T, VBF_K3, VBF_K3_SPLIT): the last one splits k_seg_or's last round of
     # segments over several workgroups (m = 2_999_999_999: 2 862 segments)
     combos = (("0", "0", "0", "1"), ("1", "1", "0", "0"), ("1", "0", "3", "1"), ("0", "1", "1", "1"),
-              ("1", "1", "4", "1"), ("-1", "1", "12", "0"), ("0", "0", "10", "1"))
+              ("1", "1", "4", "1"), ("-1", "1", "12", "0"), ("0", "0", "10", "1"), ("1", "1", "13", "1"))
     for k1, et, k3, sp in combos:
         env = {kk: vv for kk, vv in os.environ.items() if kk != "VBF_LIB"}
         env["VBF_K1"], env["VBF_ENDS_T"], env["VBF_K3"], env["VBF_K3_SPLIT"] = k1, et, k3, sp
