@@ -232,8 +232,17 @@ int vbf_filter_busy(const vbf_filter* f);
 /* Writers of the bits through vbf_filter_words_dev (an OR/merge kernel on the caller's stream)
  * bracket their work: vbf_filter_stream_wait makes `stream` wait for the filter's previous
  * operations, vbf_filter_stream_record makes the work queued on `stream` so far the filter's
- * last operation (later calls are ordered after it; the host mirror is invalidated).  A writer
- * that skips them must synchronize its stream before the next call on the filter. */
+ * last operation (later calls are ordered after it; the host mirror is refreshed behind it).
+ * Every write through the pointer must be declared with vbf_filter_stream_record: once
+ * vbf_filter_words_dev has handed the pointer out, the library no longer trusts its host mirror
+ * (host reads copy the words from the GPU each time, and migrate copies instead of assuming the
+ * words are zero) until the next vbf_filter_stream_record; a write made after that record and
+ * not recorded itself may be missed by host-side reads.  A writer that skips stream_wait must
+ * synchronize its stream before the next call on the filter.
+ * A failed asynchronous set is returned once, by the next call on the filter that waits for
+ * the queue (every call but vbf_filter_busy and the accessors).  `release` runs after the job
+ * counts as done, so it may call back into the library.  A child forked while a set is queued
+ * does not run it: the child's next call on that filter returns VBF_EINVAL. */
 int vbf_filter_stream_wait(const vbf_filter* f, void* stream);
 int vbf_filter_stream_record(vbf_filter* f, void* stream);
 /* contains over a batch (bf.rs:95-105): out[j] = 1 when every one of the k bits is set.

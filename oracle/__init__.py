@@ -40,6 +40,8 @@ def _load():
     L.ora_build_mt.argtypes = [vp, vp, u64, u64, i, u32, u32, vp, i]
     L.ora_probe.restype = i
     L.ora_probe.argtypes = [vp, vp, u64, u64, i, u32, u32, vp, vp]
+    L.ora_probe_mt.restype = i
+    L.ora_probe_mt.argtypes = [vp, vp, u64, u64, i, u32, u32, vp, vp, i]
     L.ora_hashes.restype = None
     L.ora_hashes.argtypes = [vp, vp, u64, u64, i, u32, vp]
     L.ora_splitmix64.restype = u64
@@ -113,11 +115,12 @@ def build_words(batch, m, k, words=None, threads=1):
     return words
 
 
-def probe(batch, m, k, words):
+def probe(batch, m, k, words, threads=1):
     out = np.zeros(batch.n, dtype=np.uint8)
     d, o = _ptrs(batch)
-    rc = lib.ora_probe(d, o, batch.stride, batch.n, batch.len_prefix, m, k,
-                       words.ctypes.data if words.size else None, out.ctypes.data if out.size else None)
+    args = (d, o, batch.stride, batch.n, batch.len_prefix, m, k,
+            words.ctypes.data if words.size else None, out.ctypes.data if out.size else None)
+    rc = lib.ora_probe_mt(*args, threads) if threads > 1 else lib.ora_probe(*args)
     if rc:
         raise ZeroDivisionError("m == 0 with k > 0")
     return out

@@ -51,6 +51,11 @@ int ora_build_mt(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, 
 int ora_probe(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
               int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out);
 
+/* The same answers on `threads` threads (keys split into ranges). */
+int ora_probe_mt(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                 int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                 int threads);
+
 /* Raw hashes, out[j*k + i] = calculate_hash(key_j, i). */
 void ora_hashes(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                 int len_prefix, uint32_t k, uint64_t* out);

@@ -287,3 +287,114 @@ def test_migrate_of_a_pristine_filter_moves_no_bits(vbf, ora):
     assert not f.words().any()
     f.migrate(0)
     assert not f.words().any() and not f.contains(keys[0])
+
+
+def test_multi_probe_does_not_deadlock_behind_queued_sets(vbf, ora):
+    """a multi-probe over filters whose asynchronous sets sit in one device's
+    FIFO worker in the order B, A.  The probe must not wait for A's job while holding B's lock
+    (the worker runs B's job first, under B's lock).  A long job on a third filter keeps B and
+    A queued while the probe takes its locks.  The answers equal the oracle's."""
+    from velarixdb_amd.key_range import SstRange, candidates
+    from velarixdb_amd.keys import HostBatch, pack
+    n_long, n, L = 60_000_000, 4_000_000, 16
+    fc = vbf.BloomFilter(0.01, n_long)
+    fb = vbf.BloomFilter(0.01, n)
+    fa = vbf.BloomFilter(0.01, n)
+    hc = ora.gen_fixed(0x5EED0E00, 0, n_long, L)
+    hb = ora.gen_fixed(0x5EED0E01, 0, n, L)
+    ha = ora.gen_fixed(0x5EED0E02, 0, n, L)
+    fc.set_many_async(HostBatch(hc, None, L, n_long, 1), zero_copy=True)
+    fb.set_many_async(HostBatch(hb, None, L, n, 1), zero_copy=True)
+    fa.set_many_async(HostBatch(ha, None, L, n, 1), zero_copy=True)
+    probe = [bytes(hb[i * L:(i + 1) * L]) for i in range(20)] + [bytes(ha[i * L:(i + 1) * L]) for i in range(20)]
+    probe += [b"neg%05d" % i for i in range(40)]
+    rs = [SstRange(b"\x00", b"\xff" * 20, fa), SstRange(b"\x00", b"\xff" * 20, fb)]
+    res, errs = [], []
+
+    def run():
+        try:
+            res.append(candidates(probe, rs))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(120)
+    assert not th.is_alive(), "multi-probe deadlocked behind the queued sets"
+    assert not errs, errs
+    got = res[0]
+    for col, (f, h) in enumerate(((fa, ha), (fb, hb))):
+        w = _oracle_words(ora, 0x5EED0E02 if f is fa else 0x5EED0E01, n, f.num_bits(), f.no_of_hash_func)
+        assert np.array_equal(f.words(), w)
+        want = ora.probe(pack(probe), f.num_bits(), f.no_of_hash_func, w).astype(bool)
+        assert np.array_equal(got[:, col], want), col
+    fc.sync()
+
+
+def test_external_write_without_record_is_seen(vbf, ora):
+    """bits written through words_dev_ptr and only synchronised (no
+    stream_record) are still seen by the host paths -- contains from the mirror, words -- and by
+    migrate, even when the filter was pristine (nothing set through the API)."""
+    from velarixdb_amd import HOST
+    from velarixdb_amd._lib import call
+    from velarixdb_amd.keys import HostBatch, pack
+    m, k, n, L = 1_000_003, 7, 50_000, 16
+    ka = ora.gen_fixed(0x5EED0E10, 0, n, L)
+    kb = ora.gen_fixed(0x5EED0E11, 0, n, L)
+    bb = HostBatch(kb, None, L, n, 1)
+    dev_b = torch.from_numpy(kb).to("cuda:0")
+    for pristine in (False, True):
+        f = vbf.BloomFilter.sized(m, k)
+        if not pristine:
+            f.set_batch(HostBatch(ka, None, L, n, 1))
+            assert f.contains_batch(HostBatch(ka[:L * 100], None, L, 100, 1)).all()  # fills the mirror
+            assert not f.contains_batch(HostBatch(kb[:L * 100], None, L, 100, 1)).all()
+        ptr = ctypes.c_void_p(f.words_dev_ptr())
+        s = torch.cuda.Stream()
+        # an external writer: the raw build kernel ORs B's keys into the filter's words
+        call("vbf_build_dev", _vp(dev_b), None, L, n, 1, m, k, ptr, ctypes.c_void_p(s.cuda_stream))
+        s.synchronize()  # ... and no vbf_filter_stream_record
+        want = ora.build_words(bb, m, k)
+        if not pristine:
+            ora.build_words(HostBatch(ka, None, L, n, 1), m, k, words=want)
+        assert f.contains_batch(HostBatch(kb[:L * 100], None, L, 100, 1)).all()
+        assert np.array_equal(f.words(), want)
+        f.migrate(HOST)
+        assert np.array_equal(f.words(), want)
+        f.migrate(0)
+        assert np.array_equal(f.words(), want)
+        assert f.contains_many([bytes(kb[:L])]).all()
+
+
+def test_async_set_failure_reported_by_next_call(vbf, ora):
+    """a queued set that fails on the GPU side (here the staging allocation
+    for one key claimed to be 2^40 bytes long: the device has no such memory) is reported by the
+    next call on the filter -- vbf_filter_sync -- and only once; the release callback still runs;
+    the filter keeps working and its bits are unchanged."""
+    from velarixdb_amd._lib import VbfError, call
+    from velarixdb_amd.keys import HostBatch
+    n, L = 100_000, 16
+    host = ora.gen_fixed(0x5EED0E20, 0, n, L)
+    f = vbf.BloomFilter(0.01, n)
+    f.set_batch(HostBatch(host, None, L, n, 1))
+    before = f.words()
+    released = threading.Event()
+    CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    cb = CB(lambda ctx: released.set())
+    buf = np.zeros(64, np.uint8)
+    offs = np.array([0, 1 << 40], dtype=np.uint64)
+    call("vbf_filter_set_host_async", f._h, buf.ctypes.data, offs.ctypes.data, 0, 1, 1,
+         ctypes.cast(cb, ctypes.c_void_p), 7)
+    with pytest.raises(VbfError) as ei:
+        call("vbf_filter_sync", f._h)
+    assert "asynchronous set" in str(ei.value)
+    assert released.wait(10)
+    call("vbf_filter_sync", f._h)  # reported once
+    assert np.array_equal(f.words(), before)
+    assert f.contains_batch(HostBatch(host[:L * 1000], None, L, 1000, 1)).all()
+    # the same failure reaches a contains queued behind it
+    call("vbf_filter_set_host_async", f._h, buf.ctypes.data, offs.ctypes.data, 0, 1, 1,
+         ctypes.cast(cb, ctypes.c_void_p), 8)
+    with pytest.raises(VbfError):
+        f.contains_batch(HostBatch(host[:L], None, L, 1, 1))
+    assert f.contains_batch(HostBatch(host[:L], None, L, 1, 1)).all()

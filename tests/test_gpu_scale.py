@@ -1,9 +1,13 @@
 """Headline-size checks (BASELINE configs 2, 3 and 5's sizing) on one MI355X.
 
-Config 2 is compared bit for bit with the multi-threaded oracle (16 host threads, ~40 s);
-the others through size-independent properties: the two build strategies agree, builds are
-idempotent and order-independent (OR is commutative), every inserted key is found, and the
-fill ratio matches 1 - exp(-k n / m).
+Every BASELINE shape is compared bit for bit with the multi-threaded oracle (16 host threads):
+config 2 (100M x 16 B, k = 10 and the reference's default k = 19), config 3 (100M Zipf keys:
+the words of the full build AND every answer of the 50M negative probes), config 4's shard 0
+and config 5's per-rank shape (125M x 32 B at m = 2^32 - 1, k = 4); config 5's false-positive
+rate at its full 1B-key size is the oracle's exact count over 10M negatives.  On top of that,
+size-independent properties: the two build strategies agree, builds are idempotent and
+order-independent (OR is commutative), every inserted key is found, and the fill ratio
+matches 1 - exp(-k n / m).
 """
 import ctypes
 import math
@@ -101,11 +105,10 @@ def test_config4_shard0_fresh_bit_exact(vbf, ora):
     assert np.array_equal(words.cpu().numpy().view(np.uint32), want)
 
 
-def test_config5_rank_shape_fresh(vbf):
+def test_config5_rank_shape_fresh(vbf, ora):
     """Config 5's per-rank shape on 8 GPUs: 125M x 32 B keys (1/8 of 1B), the saturated
-    m = 2^32 - 1 and k = 4 of the whole filter, a fresh partitioned build into garbage equal to
-    the per-key atomic build into zeros (the oracle would take minutes at this size; config 5's
-    sizing slice and the 5M-key oracle checks pin the 32-byte hash)."""
+    m = 2^32 - 1 and k = 4 of the whole filter: a fresh partitioned build into garbage equals
+    the per-key atomic build into zeros and the 16-thread oracle over all 125M keys."""
     from velarixdb_amd.workloads import SEED_CFG5, fpr_for_bits_per_key
     N = 1_000_000_000
     m = vbf.num_bits(N, fpr_for_bits_per_key(15))
@@ -122,13 +125,54 @@ def test_config5_rank_shape_fresh(vbf):
     assert count(vbf, keys, None, L, n, m, k, w_fresh) == n
     fill = popcount(vbf, w_fresh) / m
     assert abs(fill - (1 - math.exp(-k * n / m))) < 1e-3
+    from velarixdb_amd.keys import HostBatch
+    host = keys.cpu().numpy()
+    del keys, w_atom
+    want = ora.build_words(HostBatch(host, None, L, n, 1), m, k, threads=16)
+    assert np.array_equal(w_fresh.cpu().numpy().view(np.uint32), want)
+
+
+@pytest.mark.timeout(600)
+def test_config5_full_size_fpr_vs_oracle(vbf, ora):
+    """Config 5 at its full size on one GPU (the bench's --config 5 workload): 1B x 32 B keys,
+    m = 2^32 - 1, k = 4 ("false-positive rate matched to reference", BASELINE.json configs[4]).
+    The GPU's answers for 10M negatives (bench.py's negative set) equal the oracle's contains
+    (bf.rs:95-105) over the same words key for key, so the FPR is the reference's exact count,
+    and it sits at the rate the saturated sizing gives (fill^k)."""
+    from velarixdb_amd.keys import HostBatch
+    from velarixdb_amd.workloads import SEED_CFG5, fpr_for_bits_per_key
+    N, L = 1_000_000_000, 32
+    m = vbf.num_bits(N, fpr_for_bits_per_key(15))
+    k = vbf.num_hash_functions(m, N)
+    assert (m, k) == (4294967295, 4)
+    keys = torch.empty(N * L, dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG5, 0, N, L, vp(keys), sp())
+    words = torch.randint(-2**31, 2**31 - 1, ((m + 31) // 32,), dtype=torch.int32, device=DEV)
+    build(vbf, keys, None, L, N, m, k, 2 | FRESH, words=words)
+    del keys
+    nn = 10_000_000
+    nk = torch.empty(nn * L, dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG5 ^ 0xFF, N, nn, L, vp(nk), sp())  # bench.py rank 0
+    out = torch.empty(nn, dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_probe_dev", vp(nk), None, L, nn, 1, m, k, vp(words), vp(out), sp())
+    fp = count(vbf, nk, None, L, nn, m, k, words)
+    fill = popcount(vbf, words) / m
+    got = out.cpu().numpy()
+    host_neg = nk.cpu().numpy()
+    assert np.array_equal(host_neg, ora.gen_fixed(SEED_CFG5 ^ 0xFF, N, nn, L))
+    want = ora.probe(HostBatch(host_neg, None, L, nn, 1), m, k, words.cpu().numpy().view(np.uint32), threads=16)
+    assert np.array_equal(got, want)
+    assert fp == int(want.sum())
+    assert abs(fp / nn - fill ** k) < 1e-3
+    assert 0.130 < fp / nn < 0.140  # 1 - e^(-4 * 1e9 / 2^32) = 0.606 fill, ^4 = 0.1349
 
 
 @pytest.mark.timeout(600)
 def test_k19_full_size_bit_exact(vbf, ora):
     """The reference's default p = 1e-4 gives k = 19 (consts/mod.rs:17, bf.rs:236-239): config 2's
-    100M keys at 19 bits per key (m = 1.9e9), built with two lanes per key (vbf_partition.hpp
-    build_spl), bit-exact against the atomic build and the 16-thread oracle over all 100M keys."""
+    100M keys at 19 bits per key (m = 1.9e9), built by the default k = 19 build shape (one lane
+    per key, vbf_partition.hpp k1_shape), bit-exact against the atomic build and the 16-thread
+    oracle over all 100M keys."""
     from velarixdb_amd.keys import HostBatch
     from velarixdb_amd.workloads import SEED_CFG2, fpr_for_bits_per_key
     n, L = 100_000_000, 16
@@ -155,7 +199,7 @@ def test_k19_full_size_bit_exact(vbf, ora):
     assert np.array_equal(w_part.cpu().numpy().view(np.uint32), want)
 
 
-def test_config3_full_size_properties(vbf, ora):
+def test_config3_full_size_bit_exact(vbf, ora):
     from velarixdb_amd.keys import pack_offsets
     from velarixdb_amd.workloads import SEED_CFG3, SEED_CFG3_NEG, fpr_for_bits_per_key, var_offsets
     n = 100_000_000
@@ -175,21 +219,32 @@ def test_config3_full_size_properties(vbf, ora):
     assert torch.equal(w_fresh, w_part)
     del w_fresh
     assert count(vbf, keys, off, 0, n, m, k, w_part) == n
-    # 50M negatives: FPR near theory (fill^k) -- the reference's probabilistic contract
+    # bit-exact vs the 16-thread oracle over all 100M keys
+    data = keys.cpu().numpy()
+    del keys, off
+    wh = w_part.cpu().numpy().view(np.uint32)
+    want = ora.build_words(pack_offsets(data, off_h), m, k, threads=16)
+    assert np.array_equal(wh, want)
+    del data
+    # 50M negatives (bench.py --config 3's probe set): every answer, both probe strategies, equals
+    # the oracle's contains over the same words; the FPR is near theory (fill^k)
     nn = 50_000_000
     noff_h = var_offsets(SEED_CFG3_NEG, 0, nn)
     noff = torch.from_numpy(noff_h.view(np.int64)).to(DEV)
     nkeys = torch.empty(int(noff_h[-1]), dtype=torch.uint8, device=DEV)
     vbf._lib.call("vbf_gen_var_dev", SEED_CFG3_NEG, 0, nn, vp(noff), vp(nkeys), sp())
     fp = count(vbf, nkeys, noff, 0, nn, m, k, w_part)
+    answers = {}
+    for strat in (1, 2):
+        o = torch.empty(nn, dtype=torch.uint8, device=DEV)
+        vbf._lib.call("vbf_probe_dev_ex", vp(nkeys), vp(noff), 0, nn, 1, m, k, vp(w_part), vp(o), strat, sp())
+        answers[strat] = o.cpu().numpy()
+    ora_ans = ora.probe(pack_offsets(nkeys.cpu().numpy(), noff_h), m, k, wh, threads=16)
+    assert np.array_equal(answers[1], ora_ans)
+    assert np.array_equal(answers[2], ora_ans)
+    assert fp == int(ora_ans.sum())
     fill = popcount(vbf, w_part) / m
     assert abs(fp / nn - fill ** k) < 5e-4
-    # bit-exact vs the oracle on the first 5M keys (a filter of its own)
-    ns = 5_000_000
-    sub = build(vbf, keys, off[: ns + 1], 0, ns, 50_000_000, k, 2)
-    data = keys[: int(off_h[ns])].cpu().numpy()
-    want = ora.build_words(pack_offsets(data, off_h[: ns + 1]), 50_000_000, k, threads=16)
-    assert np.array_equal(sub.cpu().numpy().view(np.uint32), want)
 
 
 def test_config5_sizing_slice(vbf, ora):

@@ -128,6 +128,19 @@ def test_mt_build_matches_serial(ora):
     a = ora.build_words(b, m, k)
     c = ora.build_words(b, m, k, threads=4)
     assert np.array_equal(a, c)
+    # the threaded probe (the checker of the full-size GPU probes) answers like the serial one,
+    # on positives and negatives, fixed and variable-length keys, with and without the prefix
+    negs = ora.gen_fixed(0x5EED00FF, 0, 20000, 16)
+    both = pack_offsets(np.concatenate([keys, negs]), np.arange(0, 40001 * 16, 16, dtype=np.uint64))
+    want = ora.probe(both, m, k, a)
+    assert want[:20000].all() and 0 < want[20000:].sum() < 400
+    assert np.array_equal(ora.probe(both, m, k, a, threads=7), want)
+    from velarixdb_amd.workloads import var_offsets
+    off = var_offsets(0x5EED0003, 0, 3000)
+    vb = pack_offsets(ora.gen_var(0x5EED0003, 0, off), off, 0)
+    w = ora.build_words(vb, 30011, 7, threads=3)
+    assert np.array_equal(w, ora.build_words(vb, 30011, 7))
+    assert np.array_equal(ora.probe(vb, 30011, 7, w, threads=5), ora.probe(vb, 30011, 7, w))
 
 
 def test_m_zero_panics_like_reference(ora):

@@ -572,6 +572,7 @@ struct Storage {
     // stay ordered as the reference's Mutex orders them; a failed job's status is reported by the
     // next call that drains.
     uint64_t jobs_queued = 0, jobs_done = 0;
+    pid_t jobs_pid = 0;  // the process whose worker runs the queued jobs (a forked child has none)
     std::condition_variable jobs_cv;
     int async_rc = VBF_OK;
     std::string async_msg;
@@ -586,6 +587,11 @@ struct Storage {
     bool pristine = true;
     uint32_t* mirror = nullptr;
     bool mirror_ok = false;
+    // vbf_filter_words_dev handed out d_words: a caller kernel may write the bits behind the
+    // library's back, so the mirror is not trusted (every host read copies the words again) until
+    // the caller declares its write with vbf_filter_stream_record.
+    bool ext_write = false;
+    bool mirror_current() const { return mirror_ok && !ext_write; }
     bool host() const { return device == VBF_DEVICE_HOST; }
     void free_mirror() {
         if (mirror) (void)hipHostFree(mirror);
@@ -606,10 +612,26 @@ struct Storage {
     }
 };
 
+// Caller holds s.mu: true when every queued asynchronous job has run.  Jobs queued by the parent
+// of a forked child never run in the child (the worker thread stayed in the parent): the child
+// counts them as failed instead of waiting for them forever.
+bool storage_jobs_settled(Storage& s) {
+    if (s.jobs_done == s.jobs_queued) return true;
+    if (s.jobs_pid != getpid()) {
+        s.jobs_done = s.jobs_queued;
+        if (s.async_rc == VBF_OK) {
+            s.async_rc = VBF_EINVAL;
+            s.async_msg = "the process forked while an asynchronous set was queued; its bits are not in this copy";
+        }
+        return true;
+    }
+    return false;
+}
+
 // Caller holds `lk` on s.mu: waits until every asynchronous set_host job queued on the filter
 // has run (the worker takes s.mu to run one, the wait releases it), then reports a failed job.
 int storage_drain(Storage& s, std::unique_lock<std::mutex>& lk) {
-    s.jobs_cv.wait(lk, [&] { return s.jobs_done == s.jobs_queued; });
+    s.jobs_cv.wait(lk, [&] { return storage_jobs_settled(s); });
     if (s.async_rc != VBF_OK) {
         const int rc = s.async_rc;
         const std::string m = s.async_msg;
@@ -760,7 +782,7 @@ int filter_stream(int device, hipStream_t* out) {
 int mirror_fill(Storage& s) {
     int rc = storage_sync(s);
     if (rc) return rc;
-    if (s.mirror_ok || !s.nwords) return VBF_OK;
+    if (s.mirror_current() || !s.nwords) return VBF_OK;
     if (!s.mirror) HIP_TRY(hipHostMalloc((void**)&s.mirror, s.nwords * 4, hipHostMallocDefault));
     hipStream_t fs;
     if ((rc = filter_stream(s.device, &fs))) return rc;
@@ -1010,13 +1032,15 @@ class AsyncQueue {
                 q_.erase(q_.begin());
             }
             run(*j);
-            if (j->release) j->release(j->ctx);
             Storage& s = *j->s;
             {
                 std::lock_guard<std::mutex> lk(s.mu);
                 ++s.jobs_done;
             }
             s.jobs_cv.notify_all();
+            // after the job counts as done: a release callback may call back into the library
+            // (vbf_filter_sync, or a free in a Rust Drop) without waiting for its own job
+            if (j->release) j->release(j->ctx);
             delete j;
         }
     }
@@ -1444,8 +1468,16 @@ int vbf_filter_device(const vbf_filter* f) {
 }
 uint32_t* vbf_filter_words_dev(const vbf_filter* f) {
     if (!f) return nullptr;
-    std::lock_guard<std::mutex> lk(f->bits->mu);
-    return f->bits->d_words;
+    Storage& s = *f->bits;
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (s.d_words) {
+        // the caller may write through the pointer: the bits are no longer known to be zero, and
+        // the host mirror is bypassed until the write is declared (vbf_filter_stream_record)
+        s.pristine = false;
+        s.mirror_ok = false;
+        s.ext_write = true;
+    }
+    return s.d_words;
 }
 
 int vbf_filter_set_num_elements(vbf_filter* f, uint32_t n) {
@@ -1552,6 +1584,7 @@ int vbf_filter_set_host_async(vbf_filter* f, const uint8_t* keys, const uint64_t
         if (release) release(release_ctx);
     } else {
         ++s.jobs_queued;
+        s.jobs_pid = getpid();
         s.pristine = false;
         // s.device cannot change while the job is queued: migrate drains first
         AsyncQueue::get(s.device).push(j.release());
@@ -1577,7 +1610,7 @@ int vbf_filter_busy(const vbf_filter* f) {
     if (!f) return fail(VBF_EINVAL, "filter is NULL");
     Storage& s = *f->bits;
     std::lock_guard<std::mutex> lk(s.mu);
-    if (s.jobs_done != s.jobs_queued) return 1;
+    if (!storage_jobs_settled(s)) return 1;
     if (s.host() || !s.pending) return 0;
     DEVICE_SCOPE(s.device);
     const hipError_t e = hipEventQuery(s.last);
@@ -1607,6 +1640,7 @@ int vbf_filter_stream_record(vbf_filter* f, void* stream) {
     if (s.host()) return host_resident("vbf_filter_stream_record");
     DEVICE_SCOPE(s.device);
     s.pristine = false;
+    s.ext_write = false;  // the write is declared: the mirror is refreshed behind it from here on
     if ((rc = storage_mark(s, (hipStream_t)stream))) return rc;
     if ((rc = mirror_after_write(s, (hipStream_t)stream))) return rc;
     return ok();
@@ -1729,7 +1763,7 @@ static int words_to_host_locked(Storage& s, uint32_t* out) {
     DEVICE_SCOPE(s.device);
     int rc = storage_sync(s);  // this filter's pending work only: other filters keep running
     if (rc) return rc;
-    if (s.mirror_ok) {  // current host copy: no PCIe transfer
+    if (s.mirror_current()) {  // current host copy: no PCIe transfer
         par_memcpy(out, s.mirror, s.nwords * 4);
         return VBF_OK;
     }
@@ -2115,7 +2149,7 @@ int vbf_filter_rebuild_from_sst_host(vbf_filter* f, const uint8_t* data, uint64_
 namespace {
 // Locks every distinct storage of `filters` in address order (clones share one), so two
 // concurrent multi-probes over overlapping sets cannot deadlock; then drains each filter's
-// queued asynchronous sets (a worker needs only its own filter's lock, which the wait releases).
+// queued asynchronous sets.
 struct MultiLock {
     std::vector<std::unique_lock<std::mutex>> locks;
     std::vector<Storage*> v;
@@ -2126,7 +2160,28 @@ struct MultiLock {
         v.erase(std::unique(v.begin(), v.end()), v.end());
         for (Storage* st : v) locks.emplace_back(st->mu);
     }
+    // A device's worker runs its queued jobs in order, each under its own filter's lock.  Waiting
+    // for filter A's job while holding B's lock would deadlock when B's job is queued ahead of
+    // A's on the same worker.  So: with every lock held, find a filter whose jobs are
+    // not all done; if there is one, release every lock, wait for that filter alone, take the
+    // locks again (address order) and look again.  Only once all are settled are failures
+    // reported (storage_drain no longer waits then).
     int drain() {
+        for (;;) {
+            Storage* behind = nullptr;
+            for (Storage* st : v)
+                if (!storage_jobs_settled(*st)) {
+                    behind = st;
+                    break;
+                }
+            if (!behind) break;
+            for (auto& l : locks) l.unlock();
+            {
+                std::unique_lock<std::mutex> lk(behind->mu);
+                behind->jobs_cv.wait(lk, [&] { return storage_jobs_settled(*behind); });
+            }
+            for (auto& l : locks) l.lock();
+        }
         for (size_t i = 0; i < v.size(); ++i)
             if (int rc = storage_drain(*v[i], locks[i])) return rc;
         return VBF_OK;
@@ -2142,12 +2197,19 @@ int cmp_host(const uint8_t* a, uint64_t la, const uint8_t* b, uint64_t lb) {
 
 // The read path's small batches (one get: one key against every in-range SST,
 // range.rs:101-136) answered on the CPU from the filters' host mirrors; the same answers as the
-// k_multi_probe kernel.  Caller holds every filter's lock (drained), on their device.
+// k_multi_probe kernel.  Caller holds every filter's lock (drained).  The filters may live on
+// different GPUs (compaction places them round-robin, VBF_DEVICE_AUTO): each mirror is filled on
+// its own device.
+static int mirror_fill_on_device(Storage& s) {
+    DEVICE_SCOPE(s.device);
+    return mirror_fill(s);
+}
+
 int multi_probe_mirror(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
                        uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
                        const uint64_t* bounds_off, uint8_t* out) {
     for (uint32_t i = 0; i < nsst; ++i)
-        if (int rc = mirror_fill(*filters[i]->bits)) return rc;
+        if (int rc = mirror_fill_on_device(*filters[i]->bits)) return rc;
     for (uint64_t j = 0; j < n; ++j) {
         const uint8_t* kp;
         uint64_t kl;
@@ -2315,44 +2377,18 @@ int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t s
     return ok();
 }
 
-int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
-                         uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
-                         const uint64_t* bounds_off, uint8_t* out) {
-    int rc = check_keys(keys, offsets, stride, n);
-    if (rc) return rc;
-    if (!nsst || !n) {
-        if ((rc = multi_probe(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out, nullptr)))
-            return rc;
-        return ok();
-    }
-    if (!filters || !filters[0]) return fail(VBF_EINVAL, "filters is NULL");
-    if (!out) return fail(VBF_EINVAL, "out is NULL");
-    MultiLock lk(filters, nsst);
-    if ((rc = lk.drain())) return rc;
-    if (filters[0]->bits->host()) return host_resident("vbf_multi_probe_host");
-    const int device = filters[0]->bits->device;
+}  // extern "C"
+
+namespace {
+// The device path of vbf_multi_probe_host for filters that all live on `device`: the keys are
+// staged to it and the answers copied back.  Caller holds every filter's lock (drained).
+int multi_probe_host_device(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                            int len_prefix, uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
+                            const uint64_t* bounds_off, uint8_t* out, int device) {
     DEVICE_SCOPE(device);
-    bool mirrored = n <= mirror_max_keys();
-    for (uint32_t i = 0; i < nsst && mirrored; ++i) {
-        if (!filters[i]) return fail(VBF_EINVAL, "filters[%u] is NULL", i);
-        const Storage& st = *filters[i]->bits;
-        if (st.host()) return host_resident("vbf_multi_probe_host");
-        if (st.device != device)
-            return fail(VBF_EINVAL, "filters[%u] lives on device %d, filters[0] on %d", i, st.device, device);
-        if (mirror_mode(st) == VBF_MIRROR_OFF) mirrored = false;
-    }
-    if (mirrored) {
-        if (bounds_off) {
-            for (uint32_t i = 0; i < 2 * nsst; ++i)
-                if (bounds_off[i + 1] < bounds_off[i]) return fail(VBF_EINVAL, "bounds_off not nondecreasing at %u", i);
-            if (bounds_off[2 * nsst] && !bounds) return fail(VBF_EINVAL, "bounds is NULL");
-        }
-        if ((rc = multi_probe_mirror(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out)))
-            return rc;
-        return ok();
-    }
     hipStream_t s;
-    if ((rc = filter_stream(device, &s))) return rc;
+    int rc = filter_stream(device, &s);
+    if (rc) return rc;
     const uint64_t kbytes = offsets ? offsets[n] - offsets[0] : n * stride;
     const uint64_t o_off = align256(kbytes), o_out = o_off + align256(offsets ? (n + 1) * 8 : 0);
     void* ws = nullptr;
@@ -2373,6 +2409,83 @@ int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t 
         return rc;
     HIP_TRY(hipMemcpyAsync(out, d_out, n * nsst, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    return VBF_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
+                         uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
+                         const uint64_t* bounds_off, uint8_t* out) {
+    int rc = check_keys(keys, offsets, stride, n);
+    if (rc) return rc;
+    if (!nsst || !n) {
+        if ((rc = multi_probe(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out, nullptr)))
+            return rc;
+        return ok();
+    }
+    if (!filters) return fail(VBF_EINVAL, "filters is NULL");
+    for (uint32_t i = 0; i < nsst; ++i)
+        if (!filters[i]) return fail(VBF_EINVAL, "filters[%u] is NULL", i);
+    if (!out) return fail(VBF_EINVAL, "out is NULL");
+    if (bounds_off) {
+        for (uint32_t i = 0; i < 2 * nsst; ++i)
+            if (bounds_off[i + 1] < bounds_off[i]) return fail(VBF_EINVAL, "bounds_off not nondecreasing at %u", i);
+        if (bounds_off[2 * nsst] && !bounds) return fail(VBF_EINVAL, "bounds is NULL");
+    }
+    MultiLock lk(filters, nsst);
+    if ((rc = lk.drain())) return rc;
+    bool mirrored = n <= mirror_max_keys();
+    std::vector<int> devices;
+    for (uint32_t i = 0; i < nsst; ++i) {
+        const Storage& st = *filters[i]->bits;
+        if (st.host()) return host_resident("vbf_multi_probe_host");
+        if (mirror_mode(st) == VBF_MIRROR_OFF) mirrored = false;
+        if (std::find(devices.begin(), devices.end(), st.device) == devices.end()) devices.push_back(st.device);
+    }
+    if (mirrored) {  // the read path's one-key gets: no kernel, any mix of devices
+        if ((rc = multi_probe_mirror(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out)))
+            return rc;
+        return ok();
+    }
+    if (devices.size() == 1) {
+        if ((rc = multi_probe_host_device(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out,
+                                          devices[0])))
+            return rc;
+        return ok();
+    }
+    // filters on several GPUs: each device probes its own filters (the keys are staged to each),
+    // and its answer columns are scattered into out[n][nsst]
+    std::vector<const vbf_filter*> sub;
+    std::vector<uint32_t> cols;
+    std::vector<uint8_t> sb, tmp;
+    std::vector<uint64_t> so;
+    for (const int d : devices) {
+        sub.clear();
+        cols.clear();
+        sb.clear();
+        so.assign(1, 0);
+        for (uint32_t i = 0; i < nsst; ++i) {
+            if (filters[i]->bits->device != d) continue;
+            sub.push_back(filters[i]);
+            cols.push_back(i);
+            if (bounds_off) {  // this filter's [lo, hi) bound bytes, re-based
+                sb.insert(sb.end(), bounds + bounds_off[2 * i], bounds + bounds_off[2 * i + 1]);
+                so.push_back(sb.size());
+                sb.insert(sb.end(), bounds + bounds_off[2 * i + 1], bounds + bounds_off[2 * i + 2]);
+                so.push_back(sb.size());
+            }
+        }
+        const uint32_t ns = (uint32_t)sub.size();
+        tmp.resize(n * ns);
+        if ((rc = multi_probe_host_device(keys, offsets, stride, n, len_prefix, ns, sub.data(),
+                                          bounds_off ? sb.data() : nullptr, bounds_off ? so.data() : nullptr,
+                                          tmp.data(), d)))
+            return rc;
+        for (uint64_t j = 0; j < n; ++j)
+            for (uint32_t q = 0; q < ns; ++q) out[j * nsst + cols[q]] = tmp[j * ns + q];
+    }
     return ok();
 }
 

@@ -74,6 +74,21 @@ def _release(ctx):
 _RELEASE_PTR = ctypes.cast(_release, ctypes.c_void_p)
 
 
+@__import__("atexit").register
+def _drain_inflight():
+    """At interpreter exit, wait for the zero-copy jobs still queued: the library's worker would
+    otherwise call _release (Python code) after the interpreter is gone."""
+    import time
+    for _, f in list(_INFLIGHT.values()):
+        try:
+            lib.vbf_filter_sync(f._h)  # a failed job's status is of no use at exit
+        except Exception:  # noqa: BLE001
+            pass
+    t_end = time.monotonic() + 60
+    while _INFLIGHT and time.monotonic() < t_end:  # the callbacks run just after the jobs
+        time.sleep(0.001)
+
+
 def _raise(fn, exc):
     code = exc.code
     if code == VBF_EDIVZERO:
@@ -222,7 +237,7 @@ class BloomFilter:
         rel, ctx = None, None
         if zero_copy:
             token = next(_INFLIGHT_IDS)
-            _INFLIGHT[token] = b
+            _INFLIGHT[token] = (b, self)
             rel, ctx = _RELEASE_PTR, token
         try:
             call("vbf_filter_set_host_async", self._h, d, o, b.stride, b.n, b.len_prefix, rel, ctx)
