@@ -136,7 +136,7 @@ SQ_FILES = {10: "sq_tile_pack.json", 19: "sq_tile_pack_k19.json"}
 def pmc_sq(name, keys):
     """VALU issue busy, wait fractions and VALU lane-instructions per key of k_tile_pack from one
     rocprofv3 SQ pass (tools/pmc_sq.py) over a build of `keys` keys; the newest round's."""
-    for rnd in ("r03", "r02"):
+    for rnd in ("r04", "r03", "r02"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             with open(path) as f:
@@ -152,7 +152,7 @@ def pmc_sq(name, keys):
 def pmc_traffic(name, kernel=None):
     """HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes (the newest round's
     measurement): (one launch of `kernel` -- read + write --, one whole build, source file)."""
-    for rnd in ("r03", "r02", "r01"):
+    for rnd in ("r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             with open(path) as f:
@@ -525,8 +525,15 @@ def bench_var(ctx, args):
     mean_len = float(off_h[-1]) / n
     value = ctx.sum_over_ranks(n) * args.steps / wall
     kavg = float(np.mean(kms)) / 1e3
-    bpk = mean_len + 8 + m / (8.0 * n)
-    achieved = n * bpk / kavg / 1e9
+    bpk = mean_len + 8 + m / (8.0 * n)  # key bytes + their u64 offset + the filter's bytes
+    ph = phase_report(phases, args.steps)
+    # as config 2: algorithmic bytes of one build / the dominant kernel's mean launch
+    dom = max(ph, key=lambda q: ph[q]["ms_per_launch"] * ph[q]["launches"]) if ph else None
+    dom_s = ph[dom]["ms_per_launch"] / 1e3 if dom else kavg
+    achieved = n * bpk / dom_s / 1e9
+    traffic, traffic_build, traffic_src = (pmc_traffic("traffic_config3.json", "k_tile_pack<-1")
+                                           if n == 100_000_000 and k == 10 and args.strategy != 1
+                                           else (None, None, None))
     return {
         "metric": "Bloom build keys/s (device-resident variable-length keys)", "value": value,
         "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
@@ -536,9 +543,10 @@ def bench_var(ctx, args):
         "config": {"workload": "config3: %dM var-length keys (Zipf 8..128 B, mean %.1f B), %d bits/key (m=%d, k=%d) + %dM negative probes"
                    % (n // 10**6, mean_len, args.bits_per_key, m, k, nn // 10**6)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "partitioned build (offsets layout)",
-                     "kernel_ms": kavg * 1e3, "algorithmic_bytes_per_key": bpk,
-                     "phases": phase_report(phases, args.steps)},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_build": traffic_build,
+                     "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_s * 1e3,
+                     "build_ms": kavg * 1e3, "build_frac": n * bpk / kavg / 1e9 / HBM_PEAK_GBS,
+                     "algorithmic_bytes_per_key": bpk, "phases": ph},
         "probe": {"keys_per_s": nn / (float(np.mean(pkms)) / 1e3), "false_positives": fp,
                   "fpr": fp / nn, "kernel_ms": float(np.mean(pkms)),
                   "ms_by_strategy": time_probe_strategies(ctx, lambda st: call(

@@ -56,6 +56,15 @@ for s in $STEPS; do
     residency) run pytest_residency 600 python -u -m pytest tests/test_gpu_residency.py -x -v -m gpu --timeout 120 --timeout-method thread ;;
     dist2)  run bench_dist2 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;
     ubench) run ubench 300 ./tools/ubench ;;
+    rdflat) run rdflat 300 ./tools/rdflat ;;
+    abk1v2) run ab_k1v2_parity 900 env AB_PARITY=1 AB_ENVS="VBF_K1=2" bash tools/env_ab.sh
+            run ab_k1v2_19 600 env AB_ENVS="VBF_K1=1 VBF_K1=2 VBF_K1=1 VBF_K1=2" AB_ARGS="--bits-per-key 19" bash tools/env_ab.sh
+            run ab_k1v2_10 600 env AB_ENVS="VBF_K1=1 VBF_K1=2 VBF_K1=1 VBF_K1=2" bash tools/env_ab.sh ;;
+    benchk) for b in 7 14 23; do run bench_k$b 300 python bench.py --no-cpu-baseline --bits-per-key $b --steps 20; done ;;
+    benchkab) run ab_kclass 900 env AB_ENVS="VBF_KCLASS=0 VBF_KCLASS=1" AB_ARGS="--bits-per-key 7" bash tools/env_ab.sh
+              run ab_kclass14 600 env AB_ENVS="VBF_KCLASS=0 VBF_KCLASS=1" AB_ARGS="--bits-per-key 14" bash tools/env_ab.sh
+              run ab_kclass23 600 env AB_ENVS="VBF_KCLASS=0 VBF_KCLASS=1" AB_ARGS="--bits-per-key 23" bash tools/env_ab.sh
+              run ab_kclass12 600 env AB_ENVS="VBF_KCLASS=0 VBF_KCLASS=1" AB_ARGS="--bits-per-key 12" bash tools/env_ab.sh ;;
     counters) (cd /tmp && run counters 120 rocprofv3 -L) || exit $? ;;
     pmc1) (cd /tmp && run pmc1 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc1" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     pmc2) (cd /tmp && run pmc2 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc2" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;

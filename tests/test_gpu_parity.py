@@ -147,6 +147,38 @@ def test_build_fixed_matches_oracle(vbf, ora, L, lp, m, k, strategy):
     assert np.array_equal(gpu_probe(vbf, neg, m, k, got), ora.probe(neg, m, k, want))
 
 
+# every runtime-k class of k_tile_pack (vbf_tile_pack_rk.hpp: 5, 8, 12, 16, 21, 24, 32) at its
+# smallest and largest k, on each key layout and on both sides of m = 2^31 (the class kernels'
+# general remainder and 8-counter scan); cfg/config.rs:102-106 lets users pick any p
+RK_CASES = [(16, 1, 2_000_003, k) for k in (1, 2, 3, 5, 6, 7, 8, 11, 12, 13, 14, 16, 17, 18, 20, 21, 22, 23, 24, 25, 32)]
+RK_CASES += [(32, 1, 3_000_017, 14), (8, 1, 1_500_007, 6), (24, 1, 2_500_009, 23), (13, 1, 2_000_003, 17),
+             (None, 1, 2_000_003, 14), (None, 1, 2_000_003, 7), (None, 1, 4_000_037, 23), (None, 1, 2_000_003, 32),
+             (16, 0, 2_000_003, 14),  # no length prefix: the generic scratch-stash kernel
+             (16, 1, 2_300_000_023, 23), (16, 1, 3_999_999_979, 32), (32, 1, 2_200_000_009, 14),
+             (None, 1, 2_500_000_001, 23), (None, 1, 4_294_967_295, 6)]
+
+
+@pytest.mark.parametrize("L,lp,m,k", RK_CASES)
+def test_build_runtime_k_classes_match_oracle(vbf, ora, L, lp, m, k):
+    from velarixdb_amd.keys import HostBatch, pack_offsets
+    from velarixdb_amd.workloads import SEED_CFG3, var_offsets
+    n = 60_000
+    if L is None:
+        off = var_offsets(SEED_CFG3, 0, n)
+        b = pack_offsets(ora.gen_var(SEED_CFG3, 0, off), off, lp)
+    else:
+        b = HostBatch(ora.gen_fixed(0x5EED0101, 0, n, L), None, L, n, lp)
+    got = gpu_build(vbf, b, m, k, strategy=PARTITIONED)
+    if m > 100_000_000:  # compare the set bits
+        want_idx = np.unique((ora.hashes(b, k) % np.uint64(m)).ravel())
+        nz = np.flatnonzero(got)
+        bits = np.unpackbits(got[nz].view(np.uint8), bitorder="little").reshape(-1, 32)
+        got_idx = np.sort((nz[:, None].astype(np.uint64) * np.uint64(32) + np.arange(32, dtype=np.uint64))[bits.astype(bool)])
+        assert np.array_equal(got_idx, want_idx)
+        return
+    assert np.array_equal(got, ora.build_words(b, m, k))
+
+
 def test_config1_bit_exact(vbf, ora):
     """BASELINE config 1: 1M x 16 B, 10 bits/key -> m = 10,000,000, k = 10."""
     from velarixdb_amd import num_bits, num_hash_functions

@@ -24,339 +24,11 @@
 // Results are bit-identical to the per-key atomic kernel (OR is order-independent); the build
 // ORs into the existing words (bf.rs:89 never clears bits).
 #include "vbf_partition.hpp"
+#include "vbf_tile_pack.hpp"
+#include "vbf_tile_pack_rk.hpp"
 
 namespace vbf {
 
-
-struct PartPlan {
-    uint32_t k;
-    uint32_t R;           // hashing rounds per lane (ceil(KT / 1024))
-    uint32_t KT;          // keys per tile
-    uint32_t C;           // indices per tile (KT * k)
-    uint32_t CP;          // capacity: C rounded up to a multiple of 8 (whole groups)
-    uint32_t nseg, nseg_pad, G;
-    uint32_t tile_words;  // u32 words per tile in the workspace: 5 per group, rounded up to 4
-    uint32_t lds1;        // K1 dynamic LDS bytes
-    uint32_t stagger_lo, stagger_hi, stagger_sleeps;
-    uint32_t ablate;      // ablation builds only (VBF_ABLATE, vbf_kernels.hpp): 1 skip place+copy
-    uint32_t k3v;         // k_seg_or tile-loop variant (VBF_K3, see k_seg_or); 0 = by run length
-    uint32_t len_order;   // offsets layout: deal keys to lanes by length (VBF_LEN_ORDER, default 1)
-    uint32_t stage_keys;  // the lo16 image holds perm + (begin, length) per key (VBF_STAGE_KEYS)
-    uint32_t fresh;       // K3: the words hold no filter yet -- write the segment without reading it
-    uint32_t nsegS;       // row stride of ends[tile][seg] (nseg rounded up to 8: 16-byte rows)
-    uint32_t ntS;         // row stride of endsT[seg][tile] (tiles rounded up to 8)
-    uint32_t c16;         // K1's segment counters are u16 pairs (half the LDS: larger tiles)
-    uint32_t cnt_words;   // K1's counter words (a multiple of 4: the image stays 16-byte aligned)
-    uint32_t k1v;         // K1's workgroup shape (k1_shape; VBF_K1)
-    uint32_t ends_t;      // K1 writes the run ends transposed, endsT[seg][tile] (VBF_ENDS_T)
-    uint32_t nfull;       // K3: segments [0, nfull) one workgroup each; the rest split in P parts
-    uint32_t P;
-    uint64_t m, mu, nwords;
-};
-
-// Variable-length keys (offsets layout): a wave runs the prefix-absorb loop as long as its
-// longest key, and with Zipf lengths almost every wave holds one long key.  So the tile's keys
-// are dealt to lanes in order of length -- a counting sort on min(len / 8, 31) into perm[] in
-// LDS -- and a wave's lanes absorb similar numbers of blocks.  The build is an OR over keys, so
-// the order changes speed only.  hist[kLenBuckets] must be zero on entry; ends with a barrier.
-constexpr int kLenBuckets = 32;
-
-// With sbeg/slen (not null) the second pass also stages each key's (begin - base, length) at its
-// sorted slot, so the hashing rounds read them from LDS instead of a dependent offsets load.
-template <int BS = kPBlock>
-__device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, uint32_t nk, uint16_t* perm,
-                                             uint32_t* hist, uint32_t* sbeg = nullptr, uint32_t* slen = nullptr,
-                                             uint64_t base = 0) {
-    const uint32_t tid = threadIdx.x;
-    auto bucket = [&](uint32_t l) {
-        const uint64_t len = dk.offsets[key0 + l + 1] - dk.offsets[key0 + l];
-        return (uint32_t)std::min<uint64_t>(len >> 3, kLenBuckets - 1);
-    };
-    for (uint32_t l = tid; l < nk; l += BS) atomicAdd(&hist[bucket(l)], 1u);
-    __syncthreads();
-    if (tid < 64) {
-        const uint32_t v = tid < kLenBuckets ? hist[tid] : 0u;
-        uint32_t incl = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (tid >= (uint32_t)o) incl += y;
-        }
-        if (tid < kLenBuckets) hist[tid] = incl - v;
-    }
-    __syncthreads();
-    for (uint32_t l = tid; l < nk; l += BS) {
-        const uint64_t b = dk.offsets[key0 + l], len = dk.offsets[key0 + l + 1] - b;
-        const uint32_t pos = atomicAdd(&hist[(uint32_t)std::min<uint64_t>(len >> 3, kLenBuckets - 1)], 1u);
-        perm[pos] = (uint16_t)l;
-        if (sbeg) {
-            sbeg[pos] = (uint32_t)(b - base);
-            slen[pos] = (uint32_t)len;
-        }
-    }
-    __syncthreads();
-}
-
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-__device__ __forceinline__ void lds_add(lds_u32* p) {
-    (void)__hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint32_t lds_add_rtn(lds_u32* p) {
-    return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_add(lds_u32* p, uint32_t v) {
-    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ uint32_t lds_add_rtn(lds_u32* p, uint32_t v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Segment counters of K1.  C16 = false: one u32 per segment.  C16 = true: two u16 per word
-// (segment s in half s & 1 of word s >> 1; no half ever carries into the other: every count and
-// start is < CP <= 65535), which halves the counters' LDS -- at k = 10 (954 segments) the tile
-// then holds its three full stash rounds (3 072 keys instead of 3 020), at k = 19 (1 812
-// segments) likewise (1 536 instead of 1 472).  The half of segment s is bit 20 of the index:
-// shift = (idx >> 16) & 16.
-template <bool C16>
-__device__ __forceinline__ void seg_count(lds_u32* cnt0, uint32_t idx) {
-    if constexpr (C16) lds_add(&cnt0[idx >> (kSegBits + 1)], 1u << ((idx >> (kSegBits - 4)) & 16u));
-    else lds_add(&cnt0[idx >> kSegBits]);
-}
-template <bool C16>
-__device__ __forceinline__ uint32_t seg_rank(lds_u32* cnt0, uint32_t idx) {
-    if constexpr (C16) {
-        const uint32_t sh = (idx >> (kSegBits - 4)) & 16u;
-        return (lds_add_rtn(&cnt0[idx >> (kSegBits + 1)], 1u << sh) >> sh) & 0xFFFFu;
-    } else {
-        return lds_add_rtn(&cnt0[idx >> kSegBits]);
-    }
-}
-template <bool C16>
-__device__ __forceinline__ uint32_t seg_get(const uint32_t* cnt, uint32_t s) {
-    if constexpr (C16) return (cnt[s >> 1] >> ((s & 1u) * 16)) & 0xFFFFu;
-    else return cnt[s];
-}
-
-// The packed tile image: entry e lives in group e >> 3, 20 bytes = 5 words: words 0..3 hold the
-// group's eight u16 low halves (entry e at u16 (e >> 3) * 10 + (e & 7)), word 4 its eight 4-bit
-// nibbles (entry e at bits 4 * (e & 7)).
-constexpr uint32_t kGroupWords = 5;
-__host__ __device__ constexpr uint32_t group_words(uint32_t entries) { return (entries + 7) / 8 * kGroupWords; }
-
-// K > 0: k known at compile time (the stash and seed loops unroll, no indexed register moves);
-// K == 0: any k <= kStash at run time.  V = 0: __launch_bounds__(1024, 8): two workgroups per CU
-// (the hashing of one overlaps the other's sort), i.e. at most 64 VGPRs; the offsets-layout
-// kernels would otherwise take 80-90 and drop to one workgroup per CU.  V = 1: 512 threads, two
-// workgroups per CU at 4 waves per SIMD, 128 VGPRs (k1_shape).
-template <int FMT, bool LP, int K, bool M31, bool C16 = false, int V = 0>
-__global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile_pack(DevKeys dk, PartPlan pl,
-                                                                                      uint32_t* tiles, uint16_t* ends) {
-    constexpr int BS = V == 1 ? 512 : kPBlock;  // k1_shape(K, FMT > 0, V).bs
-    static_assert(V == 0 || K > 0, "the 512-thread shape is for compiled k");
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
-    // The per-segment counters first, at LDS address 0 (the kernel has no static LDS, so the
-    // dynamic allocation starts there; launch_build_partitioned checks it): the count and rank
-    // atomics address them through an LDS-space pointer to 0, so a counter's address is the
-    // segment number times 4 with no base to add -- one VALU instruction fewer per bit index in
-    // each of the two passes.  Then the tile image, 16-byte aligned.
-    uint32_t* cnt = smem_all;                           // nseg_pad (C16: nseg_pad / 2) words
-    lds_u32* const cnt0 = reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(0));  // == cnt
-    const uint32_t cnt_words = pl.cnt_words;
-    uint32_t* wsum = cnt + cnt_words;                   // 16
-    uint32_t* lhist = wsum + 16;                        // kLenBuckets (offsets layout)
-    uint32_t* smem = lhist + kLenBuckets;               // the image: (cnt_words + 48) * 4 % 16 == 0
-    uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // before placement: perm (offsets layout)
-    const uint32_t tid = threadIdx.x;
-    // Stagger (speed only): the second workgroup dispatched to each CU starts ~half a tile
-    // later, so the two co-resident workgroups alternate hashing (VALU) and sorting (LDS)
-    // instead of contending for the same pipe at the same time.
-    if (blockIdx.x >= pl.stagger_lo && blockIdx.x < pl.stagger_hi) {
-        for (uint32_t i = 0; i < pl.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-    for (uint32_t s = tid; s < cnt_words; s += BS) cnt[s] = 0;
-    if (FMT < 0 && tid < kLenBuckets) lhist[tid] = 0;
-    __syncthreads();
-
-    // SPL lanes per key (k1_shape): lane tid takes key slot r * (BS / SPL) + tid / SPL and
-    // seeds [KL * (tid % SPL), KL * (tid % SPL) + KL) of it
-    constexpr int SPL = K > 0 ? k1_shape(K, FMT > 0, V).spl : 1;
-    constexpr int KL = K > 0 ? k1_shape(K, FMT > 0, V).kl : 1;
-    constexpr uint32_t kKeysPerRound = BS / SPL;
-    constexpr int RMK = K > 0 ? k1_shape(K, FMT > 0, V).rounds : 1;
-    uint32_t stash[K > 0 ? RMK * KL : kStash];
-    // the tile: with ends_t, XCD-aware (blocks are dealt round-robin over the 8 XCDs; each XCD
-    // takes a contiguous range of tiles, so the endsT columns its workgroups write at one time are
-    // neighbours and fill whole L2 lines); otherwise the block number
-    uint32_t tile = blockIdx.x;
-    if (pl.ends_t) {
-        const uint32_t nwg = gridDim.x, q = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
-        tile = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + blockIdx.x / 8;
-    }
-    const uint64_t key0 = (uint64_t)tile * pl.KT;
-    const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
-    const uint32_t nk = (uint32_t)(key_end - key0);
-    // perm lives in the (not yet used) tile image; every read of it precedes the barrier below
-    const bool perm = FMT < 0 && pl.len_order;
-    // Staged keys (offsets layout, compiled k, plan says the image holds perm + 2 words per key,
-    // and the tile's bytes span < 4 GiB): (begin, length) at smem[sw0 ..) and smem[sw0 + nk ..).
-    const uint32_t sw0 = (nk + 1) / 2;
-    bool staged = false;
-    uint64_t sbase = 0;
-    if constexpr (FMT < 0) {
-        if (perm) {
-            if (K > 0 && pl.stage_keys) {
-                sbase = dk.offsets[key0];
-                staged = dk.offsets[key_end] - sbase < (1ull << 32);
-            }
-            if (staged)
-                length_order<BS>(dk, key0, nk, lo, lhist, smem + sw0, smem + sw0 + nk, sbase);
-            else
-                length_order<BS>(dk, key0, nk, lo, lhist);
-        }
-    }
-    auto key_of = [&](uint32_t slot) -> uint64_t { return key0 + (perm ? (uint32_t)lo[slot] : slot); };
-    uint32_t ns;  // wave-uniform: every lane stores R*k entries (sentinels past the end)
-    if constexpr (K > 0) {
-        constexpr int RM = RMK;
-        // One instance per round with r a compile-time constant: the stash index r*K+i stays
-        // static even where the round body holds a runtime loop (the offsets layout's absorb),
-        // which keeps LLVM from unrolling a plain `for` -- the stash then went to scratch
-        // memory (128 B per lane of scratch stores and loads per key, variable-length builds).
-        // Runtime-length layouts on the 512-thread shape (128 VGPRs): the first five source words
-        // of a lane's next-round key are loaded before this round's absorb, so they arrive while
-        // this round hashes (config 3: the absorb waited on its first loads).
-        constexpr bool PF = FMT <= 0 && V == 1;
-        auto key_span = [&](uint32_t slot, uint64_t& beg, uint64_t& len) {
-            if constexpr (FMT < 0) {
-                if (staged) {
-                    beg = sbase - dk.off_base + smem[sw0 + slot];
-                    len = smem[sw0 + nk + slot];
-                } else {
-                    const uint64_t j = key_of(slot);
-                    beg = dk.offsets[j] - dk.off_base;
-                    len = dk.offsets[j + 1] - dk.offsets[j];
-                }
-            } else {
-                beg = key_of(slot) * dk.stride;
-                len = dk.stride;
-            }
-        };
-        auto head_of = [&](uint32_t rr) -> KeyHead {
-            const uint32_t slot = rr * kKeysPerRound + tid / SPL;
-            uint64_t beg = 0, len = 0;  // no key: a zero-length head reads nothing
-            if (rr < pl.R && slot < nk) key_span(slot, beg, len);
-            return key_head_load(dk.keys, beg, len);
-        };
-        KeyHead head_cur{};
-        if constexpr (PF) head_cur = head_of(0);
-        auto round = [&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            const uint32_t slot = (uint32_t)r * kKeysPerRound + tid / SPL;
-            const uint32_t seed0 = (uint32_t)KL * (tid % SPL);
-            const bool valid = (uint32_t)r < pl.R && slot < nk;
-            Prefix p{};
-            if constexpr (PF) {
-                const KeyHead h = head_cur;
-                if constexpr (r + 1 < RM) head_cur = head_of(r + 1);
-                if (valid) p = key_prefix_head<LP>(h);
-            } else if (valid) {
-                if constexpr (FMT < 0) {
-                    uint64_t beg, len;
-                    key_span(slot, beg, len);
-                    p = key_prefix_at<LP>(dk.keys, beg, len);
-                } else {
-                    p = key_prefix<FMT, LP>(dk, key_of(slot));
-                }
-            }
-            // compile-time key lengths end the prefix on a block boundary: the seed loop shares
-            // half of its first SipRound (seed_hash, sip13.hpp)
-            SeedCtx q{};
-            if constexpr (FMT > 0) q = seed_ctx(p);
-#pragma unroll
-            for (int i = 0; i < KL; ++i) {
-                uint32_t idx = kSentinel;
-                if (valid && (SPL == 1 || seed0 + i < (uint32_t)K)) {
-                    const uint64_t h = FMT > 0 ? seed_hash(q, seed0 + i) : prefix_hash(p, seed0 + i);
-                    idx = mod_m<M31>(h, pl.m, pl.mu);
-                    seg_count<C16>(cnt0, idx);
-                }
-                stash[r * KL + i] = idx;
-            }
-        };
-        [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-            (round(std::integral_constant<int, Rs>{}), ...);
-        }(std::make_integer_sequence<int, RM>{});
-        ns = RM * KL;
-    } else {
-        ns = 0;
-        for (uint32_t r = 0; r < pl.R; ++r) {
-            const uint32_t slot = r * BS + tid;
-            const bool valid = slot < nk;
-            Prefix p{};
-            if (valid) p = key_prefix<FMT, LP>(dk, key_of(slot));
-            for (uint32_t i = 0; i < pl.k; ++i) {
-                uint32_t idx = kSentinel;
-                if (valid) {
-                    idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
-                    seg_count<C16>(cnt0, idx);
-                }
-                stash[ns++] = idx;
-            }
-        }
-    }
-    __syncthreads();
-    if constexpr (C16) block_exclusive_scan16(cnt, pl.nseg, wsum);  // run starts
-    else block_exclusive_scan(cnt, pl.nseg, wsum);
-    // the groups' nibble words start clear (ORed into below); the image held perm / staged keys
-    // until the hashing rounds ended
-    for (uint32_t g = tid; g < pl.CP / 8; g += BS) smem[g * kGroupWords + 4] = 0;
-    __syncthreads();
-    if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
-        uint32_t acc = 0;
-        for (uint32_t t = 0; t < ns; ++t) acc ^= stash[t];
-        if (acc == 0x12345678u) ends[blockIdx.x] = (uint16_t)acc;
-        return;
-    }
-    // rank + place, 8 returning LDS atomics in flight before their results are used
-    // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
-    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(RMK * KL) : (uint32_t)kStash;
-#pragma unroll
-    for (uint32_t t = 0; t < kNsMax; t += 8) {
-        if (t >= ns) break;
-        uint32_t pos[8], val[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? seg_rank<C16>(cnt0, val[q]) : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (val[q] != kSentinel) {
-                const uint32_t g = (pos[q] >> 3) * kGroupWords, e7 = pos[q] & 7;
-                lo[g * 2 + e7] = (uint16_t)val[q];
-                atomicOr(&smem[g + 4], ((val[q] >> 16) & kNibMask) << (e7 * 4));
-            }
-        }
-    }
-    __syncthreads();
-    // cnt[s] = start(s) + count(s) = the end of segment s's run.  The last group's low halves past
-    // the tile's end are whatever LDS held: every reader masks entries by the run bounds.
-    const uint32_t total = seg_get<C16>(cnt, pl.nseg - 1);
-    uint32_t* out = tiles + (uint64_t)tile * pl.tile_words;
-    const uint32_t words = group_words(total);
-    for (uint32_t w = tid * 4; w < words; w += BS * 4) {
-        if (w + 4 <= words)
-            *reinterpret_cast<uint4*>(out + w) = *reinterpret_cast<const uint4*>(smem + w);
-        else
-            for (uint32_t x = w; x < words; ++x) out[x] = smem[x];
-    }
-    if (pl.ends_t) {  // straight into endsT[seg][tile] (no transpose pass)
-        for (uint32_t s = tid; s < pl.nseg; s += BS) ends[(uint64_t)s * pl.ntS + tile] = (uint16_t)seg_get<C16>(cnt, s);
-    } else {
-        uint16_t* eo = ends + (uint64_t)tile * pl.nsegS;
-        for (uint32_t s = tid; s < pl.nseg; s += BS) eo[s] = (uint16_t)seg_get<C16>(cnt, s);
-    }
-}
 
 // ends[rows][cols] -> endsT[cols][rows], 64x64 tiles through LDS.
 __global__ __launch_bounds__(256) void k_transpose_u16(const uint16_t* in, uint16_t* out, uint32_t rows,
@@ -789,7 +461,9 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
 // workgroups per CU; one per CU only when two cannot hold a single round of keys.
 // fixed: the batch has a compile-time key length (pick_fmt > 0), which allows more stash rounds
 // for some k (build_rounds_max).
-static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
+// lp: the batch hashes the length prefix (Hash for [u8]; only such batches take the runtime-k
+// class kernels).
+static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = true) {
     PartPlan pl{};
     pl.k = k;
     pl.m = m;
@@ -799,6 +473,10 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
     // runtime k (the K = 0 kernel) keeps kStash / k rounds; compiled K values their own
     const bool ck = k == 4 || k == 9 || k == 10 || k == 19;
+    // any other k <= 32 (with the length prefix) takes a runtime-k class kernel on the 512-thread
+    // shape, its stash in registers (VBF_KCLASS = 0: the generic scratch-stash kernel, A/B)
+    static const int kcls = [] { const char* e = getenv("VBF_KCLASS"); return e ? atoi(e) : 1; }();
+    pl.kc = (!ck && kcls != 0 && lp) ? tile_pack_class(k) : 0u;
     // K1 shape (k1_shape): the 512-thread one-lane-per-key workgroups where they exist (compiled
     // k = 10 / 19, a scan of <= 4 * 512 segments), by default (profiles/r03/matrix1.log, one box:
     // k = 19 tile_sort 6.76 -> 6.24 ms; k = 10 even with packed counters, and with plain ones
@@ -806,6 +484,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     // VBF_K1 = 0 / 1 forces V = 0 / V = 1 where it exists.
     static const int k1env = [] { const char* e = getenv("VBF_K1"); return e ? atoi(e) : -1; }();
     pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : true) && (k == 10 || k == 19) && pl.nseg <= 4 * 512);
+    if (pl.kc) pl.k1v = 1;
     // packed u16 counters where they buy tile (VBF_C16 = 0 / 1 forces them off / on: A/B)
     static const int c16env = [] { const char* e = getenv("VBF_C16"); return e ? atoi(e) : -1; }();
     // measured: with the split image (runs padded, CP = C + nseg) they bought k = 10 its full
@@ -816,8 +495,8 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
     pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) &&
                         (c16env >= 0 ? c16env != 0 : (k == 19 && !pl.k1v)));
     if (!fixed && pl.c16) pl.k1v = 0;
-    const K1Shape sh = k1_shape((int)k, fixed, (int)pl.k1v);
-    const uint32_t rmax = (uint32_t)(ck ? sh.rounds : rounds_max((int)k));
+    const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : k), fixed, (int)pl.k1v);
+    const uint32_t rmax = (uint32_t)(ck || pl.kc ? sh.rounds : rounds_max((int)k));
     const uint32_t kpr = (uint32_t)sh.bs / (uint32_t)(ck ? sh.spl : 1);  // keys per round
     // K1 writes endsT[seg][tile] itself, no transpose pass (k = 19: -0.15 ms per 100M keys, k = 10
     // -0.025 ms; VBF_ENDS_T = 0 keeps the transpose)
@@ -876,10 +555,11 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true) {
 
 bool partition_supported(uint32_t m, uint32_t k) {
     if (m == 0 || k < 1 || k > (uint32_t)kStash) return false;
-    for (bool fixed : {true, false}) {
-        const PartPlan pl = make_plan(m, k, fixed);
-        if (pl.lds1 > kLdsPerCu || pl.CP > 65535) return false;
-    }
+    for (bool fixed : {true, false})
+        for (bool lp : {true, false}) {
+            const PartPlan pl = make_plan(m, k, fixed, lp);
+            if (pl.lds1 > kLdsPerCu || pl.CP > 65535) return false;
+        }
     return true;
 }
 
@@ -892,24 +572,27 @@ static uint64_t chunk_keys_for(const PartPlan& pl, uint64_t n) {
 uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     if (!partition_supported(m, k)) return 0;
     uint64_t need = 0;
-    for (bool fixed : {true, false}) {  // the larger of the two layouts' plans
-        const PartPlan pl = make_plan(m, k, fixed);
-        const uint64_t ntiles = (chunk_keys_for(pl, n) + pl.KT - 1) / pl.KT;
-        // tiles, then ends[ntiles][nsegS] and endsT[nsegS][ntiles rounded up to 8] (16-byte aligned)
-        need = std::max<uint64_t>(need, ntiles * (uint64_t)pl.tile_words * 4 + (ntiles + 8) * (uint64_t)pl.nsegS * 4 + 512);
-    }
+    for (bool fixed : {true, false})  // the largest of the layouts' plans
+        for (bool lp : {true, false}) {
+            const PartPlan pl = make_plan(m, k, fixed, lp);
+            const uint64_t ntiles = (chunk_keys_for(pl, n) + pl.KT - 1) / pl.KT;
+            // tiles, then ends[ntiles][nsegS] and endsT[nsegS][ntiles rounded up to 8] (16-byte aligned)
+            need = std::max<uint64_t>(need,
+                                      ntiles * (uint64_t)pl.tile_words * 4 + (ntiles + 8) * (uint64_t)pl.nsegS * 4 + 512);
+        }
     return need;
 }
 
 bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k) {
     if (!partition_supported(m, k) || n == 0) return false;
-    for (bool fixed : {true, false}) {
-        const PartPlan pl = make_plan(m, k, fixed);
-        const uint64_t ck = chunk_keys_for(pl, n);
-        const uint64_t ntiles = (ck + pl.KT - 1) / pl.KT;
-        const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)ntiles, (512 + pl.nseg - 1) / pl.nseg));
-        if (ck < n || G > 1) return false;
-    }
+    for (bool fixed : {true, false})
+        for (bool lp : {true, false}) {
+            const PartPlan pl = make_plan(m, k, fixed, lp);
+            const uint64_t ck = chunk_keys_for(pl, n);
+            const uint64_t ntiles = (ck + pl.KT - 1) / pl.KT;
+            const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)ntiles, (512 + pl.nseg - 1) / pl.nseg));
+            if (ck < n || G > 1) return false;
+        }
     return true;
 }
 
@@ -918,7 +601,7 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
     if (kb.n == 0 || k == 0) return hipSuccess;
     if (!partition_supported(m, k)) return hipErrorInvalidValue;
     // every chunk keeps the batch's alignment (chunks are whole tiles of keys), so one layout
-    PartPlan pl = make_plan(m, k, pick_fmt(kb.keys, kb.offsets, kb.stride) > 0);
+    PartPlan pl = make_plan(m, k, pick_fmt(kb.keys, kb.offsets, kb.stride) > 0, kb.len_prefix);
     const uint64_t chunk_keys = chunk_keys_for(pl, kb.n);
     const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
     if (ws_bytes < partition_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;
@@ -938,7 +621,11 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         pl.ntS = (ntiles + 7) & ~7u;
         hipError_t err = hipSuccess;
         phase_begin(kPhaseTileSort, s);
-        with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
+        if (pl.kc) {  // a runtime-k class kernel (its own translation unit)
+            const int fmt = pick_fmt(dk.keys, dk.offsets, dk.stride);
+            err = pl.kc <= 12 ? launch_tile_pack_class_a(fmt, dk, pl, ntiles, tiles, pl.ends_t ? endsT : ends, s)
+                              : launch_tile_pack_class_b(fmt, dk, pl, ntiles, tiles, pl.ends_t ? endsT : ends, s);
+        } else with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
             // m <= 2^31: the one-word remainder (fast_mod31); the runtime-k kernel keeps the general one
             auto pick = [&]<bool S>() {
                 if constexpr (FMT > 0 && S) {  // the 512-thread shape (make_plan: m <= 2^31)
@@ -965,7 +652,7 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                 err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
             if (err == hipSuccess)
-                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles,
+                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v == 1 ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles,
                                    pl.ends_t ? endsT : ends);
         });
         if (err != hipSuccess) return err;

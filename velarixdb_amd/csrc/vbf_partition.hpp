@@ -64,18 +64,18 @@ __host__ __device__ constexpr K1Shape k1_shape(int k, bool fixed, int v) {
     return K1Shape{kPBlock, build_spl(k, fixed), build_kl(k, fixed), build_rounds_max(k, fixed)};
 }
 
-// Exclusive scan of v[0..n) in LDS (n <= 4 * kPBlock).  EVEN: scan the counts rounded up to even
-// (the build's even-length runs) in the same pass.  One barrier: after it every wave adds up the
-// totals of the waves before it itself instead of waiting for one wave to scan them.  The caller
-// synchronises before reading v[] or reusing wsum[].
-template <bool EVEN = false>
+// Exclusive scan of v[0..n) in LDS (n <= PER * blockDim.x, blockDim.x <= kPBlock).  EVEN: scan the
+// counts rounded up to even (the build's even-length runs) in the same pass.  One barrier: after
+// it every wave adds up the totals of the waves before it itself instead of waiting for one wave
+// to scan them.  The caller synchronises before reading v[] or reusing wsum[].
+template <bool EVEN = false, int PER = 4>
 __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, uint32_t* wsum) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t loc[4];
+    uint32_t loc[PER];
     uint32_t sum = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t s = tid * 4 + q;
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t s = tid * PER + q;
         const uint32_t c = s < n ? v[s] : 0;
         loc[q] = EVEN ? (c + 1) & ~1u : c;
         sum += loc[q];
@@ -95,8 +95,8 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
     before = (uint32_t)__shfl((int)before, 0);
     uint32_t run = before + incl - sum;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t s = tid * 4 + q;
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t s = tid * PER + q;
         if (s < n) v[s] = run;
         run += loc[q];
     }

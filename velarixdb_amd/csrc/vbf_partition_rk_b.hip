@@ -1,0 +1,9 @@
+// vbf_partition_rk_b.hip -- K1 runtime-k classes 16, 21, 24 and 32 (vbf_tile_pack_rk.hpp).
+#include "vbf_tile_pack_rk.hpp"
+
+namespace vbf {
+hipError_t launch_tile_pack_class_b(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                    uint32_t* tiles, uint16_t* ends, hipStream_t s) {
+    return launch_class_impl<16, 21, 24, 32>(fmt, dk, pl, ntiles, tiles, ends, s);
+}
+}  // namespace vbf
