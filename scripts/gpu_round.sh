@@ -57,6 +57,10 @@ for s in $STEPS; do
     dist2)  run bench_dist2 300 env VBF_SHARE_DEVICE=1 VBF_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline ;;
     ubench) run ubench 300 ./tools/ubench ;;
     rdflat) run rdflat 300 ./tools/rdflat ;;
+    pmcrdflat) (cd /tmp && run pmc_rdflat 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_rdflat" -o run -- "$ROOT/tools/rdflat") || exit $? ;;
+    pmc2_3) (cd /tmp && run pmc2_3 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc2_3" -o run -- python3 "$ROOT/bench.py" --config 3 --steps 2 --warmup 1 --no-cpu-baseline --neg-keys 1000000) || exit $? ;;
+    pmc3_3) (cd /tmp && run pmc3_3 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc3_3" -o run -- python3 "$ROOT/bench.py" --config 3 --steps 2 --warmup 1 --no-cpu-baseline --neg-keys 1000000) || exit $? ;;
+    pmcsq3) (cd /tmp && run pmcsq3 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcsq3" -o run -- python3 "$ROOT/bench.py" --config 3 --steps 2 --warmup 1 --no-cpu-baseline --neg-keys 1000000) || exit $? ;;
     abk1v2) run ab_k1v2_parity 900 env AB_PARITY=1 AB_ENVS="VBF_K1=2" bash tools/env_ab.sh
             run ab_k1v2_19 600 env AB_ENVS="VBF_K1=1 VBF_K1=2 VBF_K1=1 VBF_K1=2" AB_ARGS="--bits-per-key 19" bash tools/env_ab.sh
             run ab_k1v2_10 600 env AB_ENVS="VBF_K1=1 VBF_K1=2 VBF_K1=1 VBF_K1=2" bash tools/env_ab.sh ;;

@@ -2,7 +2,9 @@
 //   g20 : the round-3 image -- 8-entry groups of 20 B (16 B of u16 low halves + the group's nibble
 //         word), read with a 16-byte and a 4-byte load per group (two load instructions);
 //   g16 : 6-entry groups of 16 B (three 20-bit entries per 64-bit half), 16-byte aligned: one
-//         16-byte load per group, never straddling a cache line.
+//         16-byte load per group, never straddling a cache line;
+//   raw20: the g20 image read as the aligned 16-byte chunks covering each run's groups, one per
+//         lane (what a reader that stages raw bytes and parses groups afterwards would load).
 // A wave takes the runs of 64 consecutive tiles of its segment; their groups are dealt to lanes
 // back to back (exclusive prefix + binary search, as in k_seg_or).  Each workgroup asks for 128 KiB
 // of LDS so one runs per CU, as k_seg_or's bitmap forces.  Reads only; the loaded words are folded
@@ -45,7 +47,8 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
         const uint32_t t = t0 + lane;
         const uint32_t v = t < ntiles ? row[t] : 0u;
         const uint32_t st = v & 0xFFFFu, en = v >> 16;
-        const uint32_t ch = en > st ? (en + GE - 1) / GE - st / GE : 0u;
+        uint32_t ch = en > st ? (en + GE - 1) / GE - st / GE : 0u;
+        if (GB == 0 && en > st) ch = ((en + 7) / 8 * 20 + 15) / 16 - (st / 8 * 20) / 16;  // 16-byte chunks
         uint32_t incl = ch;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -60,9 +63,12 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
                 if ((uint32_t)__shfl((int)excl, (int)r + sft) <= c) r += sft;
             const uint32_t rv = (uint32_t)__shfl((int)v, (int)r), rex = (uint32_t)__shfl((int)excl, (int)r);
             const uint8_t* tile = img + (uint64_t)min(t0 + r, ntiles - 1) * tile_bytes;
-            const uint32_t gi = (rv & 0xFFFFu) / GE + (c - rex);
+            const uint32_t gi = (rv & 0xFFFFu) / (GE ? GE : 8) + (c - rex);
             uint4 l;
-            if (GB == 16) {
+            if (GB == 0) {  // raw: aligned 16-byte chunks of the run's byte range (GE = 8, 20-byte groups)
+                l = *reinterpret_cast<const uint4*>(tile + ((rv & 0xFFFFu) / 8 * 20 / 16 + (c - rex)) * 16);
+                acc ^= l.x ^ l.y ^ l.z ^ l.w;
+            } else if (GB == 16) {
                 l = *reinterpret_cast<const uint4*>(tile + gi * 16);
                 acc ^= l.x ^ l.y ^ l.z ^ l.w;
             } else {
@@ -111,17 +117,18 @@ int main() {
         hipLaunchKernelGGL(k_gen, dim3((c.ntiles + 255) / 256), dim3(256), 0, 0, bnd, c.ntiles, c.nseg, c.mean, used);
         uint32_t cap = 0;
         (void)hipMemcpy(&cap, used, 4, hipMemcpyDeviceToHost);
-        for (int fmt = 0; fmt < 2; ++fmt) {
-            const uint32_t tile_bytes = fmt == 0 ? ((cap + 7) / 8 * 20 + 16 + 15) & ~15u : ((cap + 5) / 6 * 16 + 16);
+        for (int fmt = 0; fmt < 3; ++fmt) {
+            const uint32_t tile_bytes = fmt != 1 ? ((cap + 7) / 8 * 20 + 16 + 15) & ~15u : ((cap + 5) / 6 * 16 + 16);
             const uint64_t bytes = (uint64_t)c.ntiles * tile_bytes + 4096;
             uint8_t* img;
             if (hipMalloc(&img, bytes) != hipSuccess) return 1;
             (void)hipMemset(img, 1, bytes);
             for (int rep = 0; rep < 2; ++rep) {
-                const float ms = fmt == 0 ? run<8, 20>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
-                                          : run<6, 16>(img, bnd, c.ntiles, c.nseg, tile_bytes, out);
+                const float ms = fmt == 0   ? run<8, 20>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
+                                 : fmt == 1 ? run<6, 16>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
+                                            : run<8, 0>(img, bnd, c.ntiles, c.nseg, tile_bytes, out);
                 printf("%-6s %s %.3f ms  (%.1f G runs/s, %u B per tile, %.2f GB image)\n", c.name,
-                       fmt == 0 ? "g20" : "g16", ms, (double)nb / (ms * 1e-3) / 1e9, tile_bytes,
+                       fmt == 0 ? "g20" : fmt == 1 ? "g16" : "raw20", ms, (double)nb / (ms * 1e-3) / 1e9, tile_bytes,
                        (double)c.ntiles * tile_bytes / 1e9);
             }
             (void)hipFree(img);
