@@ -179,3 +179,78 @@ def test_interleaved_groups_device_large(vbf, multi_mode):
         f.contains_dev(P(keys), None, L, n, P(one))
         torch.cuda.synchronize()
         assert np.array_equal(got[:, s], one.cpu().numpy()), s
+
+
+@pytest.mark.parametrize("k_bits,L,ranged", [(10, 16, False), (19, None, True), (19, 32, False), (10, None, True)])
+def test_group_pipeline_matches_round3_pipeline_and_oracle(vbf, ora, multi_mode, k_bits, L, ranged):
+    """The round-4 group pipeline (VBF_MULTI_GP=1: the build's tile image with 2^17-byte segments,
+    per-entry result bytes, a key's results found through the pack's position table) against the
+    round-3 pipeline (VBF_MULTI_GP=0) and the oracle: k = 10 and the reference default k = 19,
+    fixed and variable-length keys, with and without key ranges, groups of 8 + 3 filters."""
+    import torch
+    from velarixdb_amd._lib import call
+    from velarixdb_amd.keys import HostBatch, pack_offsets
+    from velarixdb_amd.workloads import fpr_for_bits_per_key, var_offsets
+    n, S, per = 1_200_000, 11, 150_000
+    dev = torch.device("cuda:0")
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    if L is None:
+        off_h = var_offsets(0x5EED0F01, 0, n)
+        host = ora.gen_var(0x5EED0F01, 0, off_h)
+        hb = pack_offsets(host, off_h)
+        keys = torch.from_numpy(host).to(dev)
+        offs = torch.from_numpy(off_h.view(np.int64)).to(dev)
+        stride = 0
+        key_list = [bytes(host[off_h[j]:off_h[j + 1]]) for j in range(n)]
+    else:
+        host = ora.gen_fixed(0x5EED0F01, 0, n, L)
+        hb = HostBatch(host, None, L, n, 1)
+        keys = torch.from_numpy(host).to(dev)
+        offs, stride = None, L
+        key_list = [bytes(host[j * L:(j + 1) * L]) for j in range(n)]
+    p = fpr_for_bits_per_key(k_bits)
+    filters, words = [], []
+    for s_ in range(S):
+        f = vbf.BloomFilter(p, per)
+        lo = s_ * 90_000
+        sub = key_list[lo:lo + per]
+        f.set_many(sub)
+        filters.append(f)
+        words.append(f.words())
+    m, k = filters[0].num_bits(), filters[0].no_of_hash_func
+    assert k == k_bits and all(f.num_bits() == m for f in filters)
+    handles = (ctypes.c_void_p * S)(*[f._h.value for f in filters])
+    bounds = bounds_off = None
+    lo_hi = []
+    if ranged:
+        rng = np.random.default_rng(k_bits)
+        parts, bo = [], [0]
+        for s_ in range(S):
+            a, b = sorted(rng.choice(n, 2, replace=False))
+            lo_hi.append((key_list[a], key_list[b]) if key_list[a] <= key_list[b] else (key_list[b], key_list[a]))
+            for x in lo_hi[-1]:
+                parts.append(x)
+                bo.append(bo[-1] + len(x))
+        bounds = torch.from_numpy(np.frombuffer(b"".join(parts), np.uint8).copy()).to(dev)
+        bounds_off = np.asarray(bo, np.uint64)
+    outs = {}
+    for gp in ("1", "0"):
+        os.environ["VBF_MULTI_GP"] = gp
+        try:
+            multi_mode(0)
+            out = torch.empty(n * S, dtype=torch.uint8, device=dev)
+            call("vbf_multi_probe_dev", P(keys), P(offs), stride, n, 1, S, handles, P(bounds),
+                 bounds_off.ctypes.data if bounds_off is not None else None, P(out), None)
+            torch.cuda.synchronize()
+            outs[gp] = out.view(n, S).cpu().numpy()
+        finally:
+            os.environ.pop("VBF_MULTI_GP", None)
+    assert np.array_equal(outs["1"], outs["0"])
+    got = outs["1"]
+    sl = slice(0, n, 7)  # oracle on every 7th key
+    for s_ in range(S):
+        want = ora.probe(hb, m, k, words[s_], threads=8)[sl].astype(bool)
+        if ranged:
+            lo, hi = lo_hi[s_]
+            want &= np.array([lo <= x <= hi for x in key_list[sl]])
+        assert np.array_equal(got[sl, s_].astype(bool), want), s_

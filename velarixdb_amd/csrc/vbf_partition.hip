@@ -462,14 +462,16 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
 // fixed: the batch has a compile-time key length (pick_fmt > 0), which allows more stash rounds
 // for some k (build_rounds_max).
 // lp: the batch hashes the length prefix (Hash for [u8]; only such batches take the runtime-k
-// class kernels).
-static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = true) {
+// class kernels).  group: the multi-SST group pack (vbf_multi_part.hip) -- segments of 2^17
+// positions (bytes of 8 interleaved filters), the 512-thread shape, keys in key order.
+static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = true, bool group = false) {
     PartPlan pl{};
+    const int sb = group ? kByteSegBits : kSegBits;
     pl.k = k;
     pl.m = m;
     pl.mu = ~0ull / m;
     pl.nwords = ((uint64_t)m + 31) / 32;
-    pl.nseg = (uint32_t)(((uint64_t)m + (1u << kSegBits) - 1) >> kSegBits);
+    pl.nseg = (uint32_t)(((uint64_t)m + (1u << sb) - 1) >> sb);
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
     // runtime k (the K = 0 kernel) keeps kStash / k rounds; compiled K values their own
     const bool ck = k == 4 || k == 9 || k == 10 || k == 19;
@@ -485,6 +487,10 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     static const int k1env = [] { const char* e = getenv("VBF_K1"); return e ? atoi(e) : -1; }();
     pl.k1v = (uint32_t)((k1env >= 0 ? k1env == 1 : true) && (k == 10 || k == 19) && pl.nseg <= 4 * 512);
     if (pl.kc) pl.k1v = 1;
+    if (group) {
+        pl.kc = 0;
+        pl.k1v = 1;
+    }
     // packed u16 counters where they buy tile (VBF_C16 = 0 / 1 forces them off / on: A/B)
     static const int c16env = [] { const char* e = getenv("VBF_C16"); return e ? atoi(e) : -1; }();
     // measured: with the split image (runs padded, CP = C + nseg) they bought k = 10 its full
@@ -492,7 +498,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     // needs no run padding and holds 3 072 keys with plain counters, which then skip the packing's
     // VALU (the 512-thread k = 19 K1: 6.18 -> 6.05 ms, matrix3.log; k = 10 even).  Only the
     // 1 024-thread k = 19 shape (two lanes per key: m > 2^31) keeps them, for its 1 536-key tile.
-    pl.c16 = (uint32_t)((k == 19 || k == 4 || k == 10) &&
+    pl.c16 = (uint32_t)(!group && (k == 19 || k == 4 || k == 10) &&
                         (c16env >= 0 ? c16env != 0 : (k == 19 && !pl.k1v)));
     if (!fixed && pl.c16) pl.k1v = 0;
     const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : k), fixed, (int)pl.k1v);
@@ -546,7 +552,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     static const int k3v = [] { const char* e = getenv("VBF_K3"); return e ? atoi(e) : 0; }();
     pl.k3v = (uint32_t)k3v;
     static const int lord = [] { const char* e = getenv("VBF_LEN_ORDER"); return e ? atoi(e) : 1; }();
-    pl.len_order = (uint32_t)(lord != 0);
+    pl.len_order = (uint32_t)(lord != 0 && !group);  // the group pack's positions are in key order
     static const int stg = [] { const char* e = getenv("VBF_STAGE_KEYS"); return e ? atoi(e) : 1; }();
     // words: perm (KT u16) + begin + length (KT u32 each) inside the image's words
     pl.stage_keys = (uint32_t)(stg != 0 && (uint64_t)(pl.KT + 1) / 2 + 2ull * pl.KT <= group_words(pl.CP));
@@ -594,6 +600,46 @@ bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k) {
             if (ck < n || G > 1) return false;
         }
     return true;
+}
+
+// ---- the multi-SST group pack (vbf_multi_part.hip): K1 with 2^17-position segments ----
+bool group_pack_supported(uint64_t m, uint32_t k) {
+    if (m == 0 || m > (1ull << 28) || (k != 10 && k != 19)) return false;  // <= 2 048 segments
+    for (bool fixed : {true, false}) {
+        const PartPlan pl = make_plan((uint32_t)m, k, fixed, true, true);
+        if (pl.lds1 > kLdsPerCu / 2 || pl.CP > 65535 || pl.nseg > 4 * 512) return false;
+    }
+    return true;
+}
+
+PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed) { return make_plan(m, k, fixed, true, true); }
+
+uint32_t group_pack_slots(uint32_t k) {
+    const K1Shape sh = k1_shape((int)k, true, 1);
+    return (uint32_t)(sh.rounds * sh.kl);
+}
+
+hipError_t launch_group_pack(const KeyBatch& kb, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                             uint32_t* tiles, uint16_t* endsT, uint16_t* posv, hipStream_t s) {
+    hipError_t err = hipErrorInvalidValue;
+    if (!kb.len_prefix || (pl.k != 10 && pl.k != 19) || pl.k1v != 1 || !pl.ends_t) return err;
+    with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), true, [&]<int FMT, bool LP>() {
+        if constexpr (LP) {
+            auto fn = pl.k == 10 ? k_tile_pack<FMT, true, 10, true, false, 1, 0, kByteSegBits, true>
+                                 : k_tile_pack<FMT, true, 19, true, false, 1, 0, kByteSegBits, true>;
+            hipFuncAttributes fa{};
+            err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
+            if (err == hipSuccess && fa.sharedSizeBytes != 0) err = hipErrorInvalidKernelFile;
+            if (err == hipSuccess)
+                err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
+            if (err == hipSuccess) {
+                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(512), pl.lds1, s, dk, pl, tiles, endsT, posv);
+                err = hipGetLastError();
+            }
+        }
+    });
+    return err;
 }
 
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
@@ -653,7 +699,7 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
             if (err == hipSuccess)
                 hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v == 1 ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles,
-                                   pl.ends_t ? endsT : ends);
+                                   pl.ends_t ? endsT : ends, (uint16_t*)nullptr);
         });
         if (err != hipSuccess) return err;
         phase_end(kPhaseTileSort, s);

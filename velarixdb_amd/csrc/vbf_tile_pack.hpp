@@ -97,18 +97,20 @@ __device__ __forceinline__ uint32_t lds_add_rtn(lds_u32* p, uint32_t v) {
 // then holds its three full stash rounds (3 072 keys instead of 3 020), at k = 19 (1 812
 // segments) likewise (1 536 instead of 1 472).  The half of segment s is bit 20 of the index:
 // shift = (idx >> 16) & 16.
-template <bool C16>
+// SB: segment = 2^SB positions (the build: 2^20 filter bits; the multi-SST group pack: 2^17 bytes
+// of interleaved filters, vbf_multi_part.hip).
+template <bool C16, int SB = kSegBits>
 __device__ __forceinline__ void seg_count(lds_u32* cnt0, uint32_t idx) {
-    if constexpr (C16) lds_add(&cnt0[idx >> (kSegBits + 1)], 1u << ((idx >> (kSegBits - 4)) & 16u));
-    else lds_add(&cnt0[idx >> kSegBits]);
+    if constexpr (C16) lds_add(&cnt0[idx >> (SB + 1)], 1u << ((idx >> (SB - 4)) & 16u));
+    else lds_add(&cnt0[idx >> SB]);
 }
-template <bool C16>
+template <bool C16, int SB = kSegBits>
 __device__ __forceinline__ uint32_t seg_rank(lds_u32* cnt0, uint32_t idx) {
     if constexpr (C16) {
-        const uint32_t sh = (idx >> (kSegBits - 4)) & 16u;
-        return (lds_add_rtn(&cnt0[idx >> (kSegBits + 1)], 1u << sh) >> sh) & 0xFFFFu;
+        const uint32_t sh = (idx >> (SB - 4)) & 16u;
+        return (lds_add_rtn(&cnt0[idx >> (SB + 1)], 1u << sh) >> sh) & 0xFFFFu;
     } else {
-        return lds_add_rtn(&cnt0[idx >> kSegBits]);
+        return lds_add_rtn(&cnt0[idx >> SB]);
     }
 }
 template <bool C16>
@@ -132,9 +134,15 @@ __host__ __device__ constexpr uint32_t group_words(uint32_t entries) { return (e
 // (the hashing of one overlaps the other's sort), i.e. at most 64 VGPRs; the offsets-layout
 // kernels would otherwise take 80-90 and drop to one workgroup per CU.  V = 1: 512 threads, two
 // workgroups per CU at 4 waves per SIMD, 128 VGPRs (k1_shape).
-template <int FMT, bool LP, int K, bool M31, bool C16 = false, int V = 0, int KC = 0>
+//
+// SB < kSegBits, POS (the multi-SST group pack, vbf_multi_part.hip): segments of 2^SB positions, and
+// every entry's place in the tile image is also written to posv[tile][stash slot][lane] (u16), so
+// the group output pass finds a key's k results without re-reading the image.
+template <int FMT, bool LP, int K, bool M31, bool C16 = false, int V = 0, int KC = 0, int SB = kSegBits,
+          bool POS = false>
 __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile_pack(DevKeys dk, PartPlan pl,
-                                                                                      uint32_t* tiles, uint16_t* ends) {
+                                                                                      uint32_t* tiles, uint16_t* ends,
+                                                                                      uint16_t* posv) {
     constexpr int BS = V == 1 ? 512 : kPBlock;  // k1_shape(K, FMT > 0, V).bs
     static_assert(V == 0 || K > 0 || KC > 0, "the 512-thread shape is for compiled k and k classes");
     static_assert(KC == 0 || (K == 0 && V == 1 && !C16), "k classes run on the 512-thread shape");
@@ -265,7 +273,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
                 if (valid && (SPL == 1 || seed0 + i < (uint32_t)K) && (KC == 0 || (uint32_t)i < pl.k)) {
                     const uint64_t h = FMT > 0 ? seed_hash(q, seed0 + i) : prefix_hash(p, seed0 + i);
                     idx = mod_m<M31>(h, pl.m, pl.mu);
-                    seg_count<C16>(cnt0, idx);
+                    seg_count<C16, SB>(cnt0, idx);
                 }
                 stash[r * KL + i] = idx;
             }
@@ -285,7 +293,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
-                    seg_count<C16>(cnt0, idx);
+                    seg_count<C16, SB>(cnt0, idx);
                 }
                 stash[ns++] = idx;
             }
@@ -317,15 +325,21 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? seg_rank<C16>(cnt0, val[q]) : 0u;
+            pos[q] = val[q] != kSentinel ? seg_rank<C16, SB>(cnt0, val[q]) : 0u;
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (val[q] != kSentinel) {
                 const uint32_t g = (pos[q] >> 3) * kGroupWords, e7 = pos[q] & 7;
                 lo[g * 2 + e7] = (uint16_t)val[q];
-                atomicOr(&smem[g + 4], ((val[q] >> 16) & kNibMask) << (e7 * 4));
+                atomicOr(&smem[g + 4], ((val[q] >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4));
             }
+        }
+        if constexpr (POS) {  // coalesced: for one stash slot the lanes write consecutive u16
+            static_assert(KK > 0, "the group pack runs compiled k");
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (val[q] != kSentinel) posv[((uint64_t)tile * kNsMax + t + q) * BS + tid] = (uint16_t)pos[q];
         }
     }
     __syncthreads();
@@ -347,5 +361,15 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
         for (uint32_t s = tid; s < pl.nseg; s += BS) eo[s] = (uint16_t)seg_get<C16>(cnt, s);
     }
 }
+
+// The multi-SST group pack (vbf_partition.hip, used by vbf_multi_part.hip): k_tile_pack over
+// 2^17-position segments of an interleaved group (k = 10 or 19, keys hashed with the length prefix,
+// m <= 2^28 positions), writing the tile images, endsT[seg][tile] (row stride pl.ntS, set by the
+// caller) and every entry's place posv[tile][slot][lane] (group_pack_slots(k) slots of 512 lanes).
+bool group_pack_supported(uint64_t m, uint32_t k);
+PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed);
+uint32_t group_pack_slots(uint32_t k);
+hipError_t launch_group_pack(const KeyBatch& kb, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                             uint32_t* tiles, uint16_t* endsT, uint16_t* posv, hipStream_t s);
 
 }  // namespace vbf

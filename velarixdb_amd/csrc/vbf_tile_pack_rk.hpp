@@ -34,7 +34,7 @@ hipError_t launch_one_class(const DevKeys& dk, const PartPlan& pl, uint32_t ntil
         err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)pl.lds1);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(fn, dim3(ntiles), dim3(512), pl.lds1, s, dk, pl, tiles, ends);
+    hipLaunchKernelGGL(fn, dim3(ntiles), dim3(512), pl.lds1, s, dk, pl, tiles, ends, (uint16_t*)nullptr);
     return hipGetLastError();
 }
 
