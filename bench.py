@@ -859,7 +859,7 @@ def bench_multi(ctx, args):
     def step(evs):
         call("vbf_multi_probe_dev", vp(keys), None, L, n, 1, S, handles, None, None, vp(out), ctx.sp)
 
-    wall, _, _ = timed_steps(ctx, step, args.steps, args.warmup)
+    wall, _, phases = timed_steps(ctx, step, args.steps, args.warmup)
     hits = int(out.view(n, S).any(dim=1).sum().item())
     return {"metric": "multi-SST probe keys/s (each key tested against 8 filters, device-resident)",
             "value": ctx.sum_over_ranks(n) * args.steps / wall, "unit": "keys/s", "n_gpus": ctx.world,
@@ -867,7 +867,8 @@ def bench_multi(ctx, args):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": "%dM x 16B keys vs %d filters of 10M keys (m=1e8, k=10); %d keys hit some SST"
                        % (n // 10**6, S, hits)},
-            "probes_per_s": ctx.sum_over_ranks(n) * S * args.steps / wall}
+            "probes_per_s": ctx.sum_over_ranks(n) * S * args.steps / wall,
+            "phases": phase_report(phases, args.steps)}
 
 
 def bench_memtable(ctx, args):

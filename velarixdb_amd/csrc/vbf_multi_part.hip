@@ -263,10 +263,24 @@ __global__ __launch_bounds__(kPBlock) void k_group_seg2(const uint32_t* tiles, c
         uint8_t* dst = res + (uint64_t)t * pl.CP + gi * 8;
         if (a == 0 && b == 8) {
             *reinterpret_cast<uint2*>(dst) = make_uint2(r[0], r[1]);
-        } else {
+        } else {  // a group shared with a neighbouring run: only [a, b), in aligned pieces
+            // greedy aligned pieces (4, 2 or 1 bytes): at most four stores for any [a, b) of 8
+            const uint64_t v = (uint64_t)r[0] | ((uint64_t)r[1] << 32);
+            uint32_t c = a;
 #pragma unroll
-            for (int c = 0; c < 8; ++c)
-                if ((uint32_t)c >= a && (uint32_t)c < b) dst[c] = (uint8_t)(r[c >> 2] >> (8 * (c & 3)));
+            for (int step = 0; step < 4; ++step) {
+                if (c >= b) break;
+                if ((c & 3) == 0 && c + 4 <= b) {
+                    *reinterpret_cast<uint32_t*>(dst + c) = (uint32_t)(v >> (8 * c));
+                    c += 4;
+                } else if ((c & 1) == 0 && c + 2 <= b) {
+                    *reinterpret_cast<uint16_t*>(dst + c) = (uint16_t)(v >> (8 * c));
+                    c += 2;
+                } else {
+                    dst[c] = (uint8_t)(v >> (8 * c));
+                    c += 1;
+                }
+            }
         }
     };
     const uint32_t wstep = (kPBlock / 64) * 64;
@@ -351,7 +365,9 @@ __global__ __launch_bounds__(kPBlock) void k_group_seg2(const uint32_t* tiles, c
     }
 }
 
-// GP4: dynamic LDS = the tile's result bytes (pl.CP, a multiple of 8).
+// GP4: dynamic LDS = the tile's result bytes (pl.CP, a multiple of 8).  K compile-time: a lane
+// issues the K position loads of each of its KPT keys together (one memory latency, not K * KPT).
+template <int K, int KPT>
 __global__ __launch_bounds__(kPBlock) void k_group_out2(const uint8_t* res, const uint16_t* posv, const uint16_t* endsT,
                                                         PartPlan pl, uint32_t slots, DevKeys dk, MultiGroup g,
                                                         const uint8_t* bounds, uint8_t* out, uint32_t out_stride) {
@@ -369,10 +385,21 @@ __global__ __launch_bounds__(kPBlock) void k_group_out2(const uint8_t* res, cons
     bool packed = g.G == 8 && (out_stride & 7u) == 0 && (g.col[0] & 7u) == 0 && !bounds &&
                   (reinterpret_cast<uintptr_t>(out) & 7u) == 0;
     for (uint32_t q = 1; q < g.G && packed; ++q) packed = g.col[q] == g.col[0] + q;
-    for (uint32_t l = tid; l < nk; l += kPBlock) {
+    uint16_t p[KPT][K];
+#pragma unroll
+    for (int x = 0; x < KPT; ++x) {
+        const uint32_t l = tid + x * kPBlock;
         const uint32_t r = l >> 9, ln = l & 511u;  // stash round and lane of key l (512-thread pack)
+#pragma unroll
+        for (int i = 0; i < K; ++i) p[x][i] = l < nk ? pt[(r * K + i) * 512 + ln] : (uint16_t)0;
+    }
+#pragma unroll
+    for (int x = 0; x < KPT; ++x) {
+        const uint32_t l = tid + x * kPBlock;
+        if (l >= nk) break;
         uint32_t mk = full;
-        for (uint32_t i = 0; i < pl.k; ++i) mk &= rl[pt[(r * pl.k + i) * 512 + ln]];
+#pragma unroll
+        for (int i = 0; i < K; ++i) mk &= rl[p[x][i]];
         const uint64_t j = key0 + l;
         uint8_t* row = out + j * out_stride;
         if (packed) {
@@ -467,8 +494,10 @@ static hipError_t launch_multi_probe_gp(const KeyBatch& kb, const MultiGroup& g,
     uint16_t* posv = reinterpret_cast<uint16_t*>(base + o_pos);
     const uint64_t nwords = (g.m + 31) / 32;
     hipLaunchKernelGGL(k_interleave, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, g, nwords, bytes);
-    // k_group_out2's dynamic LDS: the tile's result bytes (up to 64 KiB)
-    hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(k_group_out2),
+    // k_group_out2's dynamic LDS: the tile's result bytes (up to 64 KiB); keys per lane: KT / 1024
+    auto out2 = g.k == 10 ? k_group_out2<10, 3> : k_group_out2<19, 2>;
+    if (pl.KT > 1024u * (g.k == 10 ? 3u : 2u)) return hipErrorInvalidValue;
+    hipError_t e0 = hipFuncSetAttribute(reinterpret_cast<const void*>(out2),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
     if (e0 != hipSuccess) return e0;
     for (uint64_t lo = 0; lo < kb.n; lo += chunk_keys) {
@@ -490,8 +519,8 @@ static hipError_t launch_multi_probe_gp(const KeyBatch& kb, const MultiGroup& g,
                            nbytes, res);
         phase_end(kPhaseProbeSeg, s);
         phase_begin(kPhaseProbeOut, s);
-        hipLaunchKernelGGL(k_group_out2, dim3(ntiles), dim3(kPBlock), (pl.CP + 15) & ~15u, s, res, posv, endsT, pl,
-                           slots, dk, g, bounds, out + lo * out_stride, out_stride);
+        hipLaunchKernelGGL(out2, dim3(ntiles), dim3(kPBlock), (pl.CP + 15) & ~15u, s, res, posv, endsT, pl, slots, dk,
+                           g, bounds, out + lo * out_stride, out_stride);
         phase_end(kPhaseProbeOut, s);
         err = hipGetLastError();
         if (err != hipSuccess) return err;
