@@ -254,3 +254,44 @@ def test_group_pipeline_matches_round3_pipeline_and_oracle(vbf, ora, multi_mode,
             lo, hi = lo_hi[s_]
             want &= np.array([lo <= x <= hi for x in key_list[sl]])
         assert np.array_equal(got[sl, s_].astype(bool), want), s_
+
+
+@pytest.mark.parametrize("m,k", [(268_434_000, 19), (5_000, 10), (40_000_003, 10)])
+def test_group_pipeline_edge_sizes(vbf, ora, multi_mode, m, k):
+    """The group pipeline at its size limits: m just under 2^28 positions (2 048 segments of
+    2^17, sparse filters: short and empty runs, the padded copy-out's binary search over empty
+    segments), one segment (m = 5 000: every tile split over many workgroups), and a mid size;
+    8 filters of one (m, k), device keys; equal to the round-3 pipeline and to the oracle."""
+    import torch
+    from velarixdb_amd._lib import call
+    from velarixdb_amd.keys import HostBatch
+    n, L, S = 1_100_000, 16, 8
+    dev = torch.device("cuda:0")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    host = ora.gen_fixed(0x5EED0F11, 0, n, L)
+    keys = torch.from_numpy(host).to(dev)
+    filters, words = [], []
+    for s_ in range(S):
+        f = vbf.BloomFilter.sized(m, k)
+        per = 200_000
+        f.set_dev(P(keys[s_ * 100_000 * L:]), None, L, per, 1)
+        filters.append(f)
+        words.append(f.words())
+    handles = (ctypes.c_void_p * S)(*[f._h.value for f in filters])
+    outs = {}
+    for gp in ("1", "0"):
+        os.environ["VBF_MULTI_GP"] = gp
+        try:
+            multi_mode(0)
+            out = torch.empty(n * S, dtype=torch.uint8, device=dev)
+            call("vbf_multi_probe_dev", P(keys), None, L, n, 1, S, handles, None, None, P(out), None)
+            torch.cuda.synchronize()
+            outs[gp] = out.view(n, S).cpu().numpy()
+        finally:
+            os.environ.pop("VBF_MULTI_GP", None)
+    assert np.array_equal(outs["1"], outs["0"])
+    sl = slice(0, n, 5)
+    hb = HostBatch(host, None, L, n, 1)
+    for s_ in range(S):
+        want = ora.probe(hb, m, k, words[s_], threads=8)[sl].astype(bool)
+        assert np.array_equal(outs["1"][sl, s_].astype(bool), want), s_

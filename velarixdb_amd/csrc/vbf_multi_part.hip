@@ -217,11 +217,12 @@ __global__ __launch_bounds__(kPBlock) void k_group_out(const uint32_t* tiles, co
 
 // ---- Round 4: the group pipeline on the build's image (k = 10 / 19 with the length prefix) ----
 // GP1 launch_group_pack (k_tile_pack with 2^17-position segments): the tile image in the build's
-// 2.5-byte 8-entry groups instead of 4-byte (key id, position) entries padded per run, the run ends
-// written transposed, and each entry's place in its tile in posv[tile][slot][lane].
+// 2.5-byte 8-entry groups instead of 4-byte (key id, position) entries, each run padded to whole
+// groups in HBM (the LDS image stays unpadded; the copy-out repacks), the padded run ends written
+// transposed, and each entry's padded place in its tile in posv[tile][slot][lane].
 // GP3 k_group_seg2: k_seg_or's flattened reader over a segment's runs, each entry answered with its
-// interleaved byte at the entry's place, res[tile][e] (one byte per entry: a group shared with the
-// neighbouring run, another workgroup's, is written byte by byte).
+// interleaved byte at the entry's place, res[tile][e]: whole groups, one 8-byte store each (runs
+// never share a group; the piecewise path for a partial group is kept for unpadded images).
 // GP4 k_group_out2: per tile, the result bytes staged in LDS; a key's k results are found through
 // posv (coalesced u16 reads) instead of re-reading and decoding every entry, then ANDed.
 template <int NG = 4>
@@ -260,7 +261,7 @@ __global__ __launch_bounds__(kPBlock) void k_group_seg2(const uint32_t* tiles, c
             const uint32_t off = ((w[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) | (((nib >> (4 * c)) & 1u) << 16);
             r[c >> 2] |= (uint32_t)sb[off] << (8 * (c & 3));
         }
-        uint8_t* dst = res + (uint64_t)t * pl.CP + gi * 8;
+        uint8_t* dst = res + (uint64_t)t * pl.CPg + gi * 8;
         if (a == 0 && b == 8) {
             *reinterpret_cast<uint2*>(dst) = make_uint2(r[0], r[1]);
         } else {  // a group shared with a neighbouring run: only [a, b), in aligned pieces
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(kPBlock) void k_group_seg2(const uint32_t* tiles, c
     }
 }
 
-// GP4: dynamic LDS = the tile's result bytes (pl.CP, a multiple of 8).  K compile-time: a lane
+// GP4: dynamic LDS = the tile's result bytes (pl.CPg, a multiple of 8).  K compile-time: a lane
 // issues the K position loads of each of its KPT keys together (one memory latency, not K * KPT).
 template <int K, int KPT>
 __global__ __launch_bounds__(kPBlock) void k_group_out2(const uint8_t* res, const uint16_t* posv, const uint16_t* endsT,
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(kPBlock) void k_group_out2(const uint8_t* res, cons
     const uint64_t key0 = (uint64_t)tile * pl.KT;
     const uint32_t nk = (uint32_t)std::min<uint64_t>(pl.KT, dk.n - key0);
     const uint32_t total = endsT[(uint64_t)(pl.nseg - 1) * pl.ntS + tile];
-    const uint2* src = reinterpret_cast<const uint2*>(res + (uint64_t)tile * pl.CP);
+    const uint2* src = reinterpret_cast<const uint2*>(res + (uint64_t)tile * pl.CPg);
     for (uint32_t w = tid; w * 8 < total; w += kPBlock) reinterpret_cast<uint2*>(rl32)[w] = src[w];
     __syncthreads();
     const uint32_t full = g.G >= 8 ? 0xFFu : ((1u << g.G) - 1u);
@@ -460,7 +461,7 @@ static uint64_t gp_workspace_bytes(uint64_t n, uint64_t m, uint32_t k) {
     for (bool fixed : {true, false}) {
         const PartPlan pl = make_group_plan((uint32_t)m, k, fixed);
         const uint64_t nt = (gp_chunk_keys(pl, n) + pl.KT - 1) / pl.KT, ntS = (nt + 7) & ~7ull;
-        need = std::max<uint64_t>(need, nt * (uint64_t)pl.tile_words * 4 + ntS * pl.nseg * 2 + nt * pl.CP +
+        need = std::max<uint64_t>(need, nt * (uint64_t)pl.tile_words * 4 + ntS * pl.nseg * 2 + nt * pl.CPg +
                                             nt * (uint64_t)group_pack_slots(k) * 512 * 2 + 4 * 256);
     }
     return need;
@@ -487,7 +488,7 @@ static hipError_t launch_multi_probe_gp(const KeyBatch& kb, const MultiGroup& g,
     const uint64_t o_tiles = align256(nbytes);
     const uint64_t o_ends = align256(o_tiles + max_tiles * pl.tile_words * 4);
     const uint64_t o_res = align256(o_ends + max_ntS * pl.nseg * 2);
-    const uint64_t o_pos = align256(o_res + max_tiles * pl.CP);
+    const uint64_t o_pos = align256(o_res + max_tiles * pl.CPg);
     uint32_t* tiles = reinterpret_cast<uint32_t*>(base + o_tiles);
     uint16_t* endsT = reinterpret_cast<uint16_t*>(base + o_ends);
     uint8_t* res = reinterpret_cast<uint8_t*>(base + o_res);
@@ -519,7 +520,7 @@ static hipError_t launch_multi_probe_gp(const KeyBatch& kb, const MultiGroup& g,
                            nbytes, res);
         phase_end(kPhaseProbeSeg, s);
         phase_begin(kPhaseProbeOut, s);
-        hipLaunchKernelGGL(out2, dim3(ntiles), dim3(kPBlock), (pl.CP + 15) & ~15u, s, res, posv, endsT, pl, slots, dk,
+        hipLaunchKernelGGL(out2, dim3(ntiles), dim3(kPBlock), (pl.CPg + 15) & ~15u, s, res, posv, endsT, pl, slots, dk,
                            g, bounds, out + lo * out_stride, out_stride);
         phase_end(kPhaseProbeOut, s);
         err = hipGetLastError();

@@ -510,9 +510,10 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     pl.ends_t = (uint32_t)(etenv != 0);
     const uint32_t cnt_words = pl.c16 ? ((pl.nseg + 7) & ~7u) / 2 : pl.nseg_pad;
     pl.cnt_words = cnt_words;
+    pl.gd_words = group ? (((pl.nseg + 1) / 2 + 3) & ~3u) : 0u;  // the group pack's u16 run table
     for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
-        const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)cnt_words;
+        const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)cnt_words - 4 * (int64_t)pl.gd_words;
         // LDS = 2.5 * CP with CP <= C + 7
         const int64_t cmax = avail * 2 / 5 - 8;
         const int64_t kt = std::min<int64_t>((int64_t)rmax * kpr, cmax / k);
@@ -524,7 +525,9 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     pl.R = (pl.KT + kpr - 1) / kpr;
     pl.C = pl.KT * k;
     pl.CP = (pl.C + 7) & ~7u;
-    pl.tile_words = (group_words(pl.CP) + 3) & ~3u;  // tiles start 16-byte aligned
+    // the group pack pads every run to whole groups in HBM (<= 7 entries per segment)
+    pl.CPg = group ? (pl.C + 7 * pl.nseg + 7) & ~7u : pl.CP;
+    pl.tile_words = (group_words(pl.CPg) + 3) & ~3u;  // tiles start 16-byte aligned
     // VBF_TILE_PAD (speed only; default 4 words): extra words per tile in the workspace, which
     // move the tile stride off large powers of two -- k_seg_or reads the runs of consecutive tiles
     // at the same offset in each, and k = 10's 76 800-byte stride is a multiple of 1 KiB (seg_or
@@ -532,7 +535,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     static const int tpad = [] { const char* e = getenv("VBF_TILE_PAD"); return e ? atoi(e) : 4; }();
     pl.tile_words += (uint32_t)std::max(0, tpad) & ~3u;
     pl.nsegS = (pl.nseg + 7) & ~7u;
-    pl.lds1 = (group_words(pl.CP) + cnt_words + 16 + kLenBuckets) * 4;
+    pl.lds1 = (group_words(pl.CP) + cnt_words + 16 + kLenBuckets + pl.gd_words) * 4;
     // VBF_TILE_LDS_MIN (experiments, speed only): request at least this much LDS per k_tile_pack
     // workgroup, e.g. > 80 KiB to hold one workgroup per CU
     static const int lds_min = [] { const char* e = getenv("VBF_TILE_LDS_MIN"); return e ? atoi(e) : 0; }();
@@ -607,7 +610,7 @@ bool group_pack_supported(uint64_t m, uint32_t k) {
     if (m == 0 || m > (1ull << 28) || (k != 10 && k != 19)) return false;  // <= 2 048 segments
     for (bool fixed : {true, false}) {
         const PartPlan pl = make_plan((uint32_t)m, k, fixed, true, true);
-        if (pl.lds1 > kLdsPerCu / 2 || pl.CP > 65535 || pl.nseg > 4 * 512) return false;
+        if (pl.lds1 > kLdsPerCu / 2 || pl.CPg > 65535 || pl.nseg > 4 * 512) return false;
     }
     return true;
 }

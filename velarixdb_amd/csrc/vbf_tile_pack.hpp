@@ -29,6 +29,8 @@ struct PartPlan {
     uint32_t k1v;         // K1's workgroup shape (k1_shape; VBF_K1)
     uint32_t ends_t;      // K1 writes the run ends transposed, endsT[seg][tile] (VBF_ENDS_T)
     uint32_t kc;          // K1 runtime-k class: k <= kc seeds per key in a kc-slot stash (0: none)
+    uint32_t gd_words;    // group pack: LDS words of its per-segment u16 table (0 for the build)
+    uint32_t CPg;         // group pack: entries per tile in HBM, every run padded to whole groups
     uint32_t nfull;       // K3: segments [0, nfull) one workgroup each; the rest split in P parts
     uint32_t P;
     uint64_t m, mu, nwords;
@@ -158,7 +160,8 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     const uint32_t cnt_words = pl.cnt_words;
     uint32_t* wsum = cnt + cnt_words;                   // 16
     uint32_t* lhist = wsum + 16;                        // kLenBuckets (offsets layout)
-    uint32_t* smem = lhist + kLenBuckets;               // the image: (cnt_words + 48) * 4 % 16 == 0
+    uint32_t* gd = lhist + kLenBuckets;                 // POS: gd_words (a multiple of 4)
+    uint32_t* smem = gd + pl.gd_words;                  // the image: (cnt_words + 48) * 4 % 16 == 0
     uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // before placement: perm (offsets layout)
     const uint32_t tid = threadIdx.x;
     // Stagger (speed only): the second workgroup dispatched to each CU starts ~half a tile
@@ -303,8 +306,32 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     // run starts; the 512-thread shape scans up to 8 counters per thread where m > 2^31
     // (up to 4 096 segments)
     constexpr int SPER = (V == 1 && !M31) ? 8 : 4;
-    if constexpr (C16) block_exclusive_scan16(cnt, pl.nseg, wsum);
-    else block_exclusive_scan<false, SPER>(cnt, pl.nseg, wsum);
+    auto gd_get = [&](uint32_t sg) -> uint32_t { return (gd[sg >> 1] >> ((sg & 1u) * 16)) & 0xFFFFu; };
+    if constexpr (POS) {
+        // every run padded to whole groups in HBM: gd = groups per segment (u16 pairs), scanned
+        // after the counters into each run's first group, then turned into the run's shift
+        // dlt(s) = 8 * gstart(s) - start(s) (< 7 * nseg) for the positions written to posv
+        static_assert(!C16, "the group pack keeps plain counters");
+        for (uint32_t w = tid; w < (pl.nseg + 1) / 2; w += BS) {
+            const uint32_t s0 = 2 * w, s1 = s0 + 1;
+            gd[w] = ((cnt[s0] + 7) >> 3) | (s1 < pl.nseg ? ((cnt[s1] + 7) >> 3) << 16 : 0u);
+        }
+        __syncthreads();
+        block_exclusive_scan<false, SPER>(cnt, pl.nseg, wsum);
+        __syncthreads();
+        block_exclusive_scan16(gd, pl.nseg, wsum);
+        __syncthreads();
+        for (uint32_t w = tid; w < (pl.nseg + 1) / 2; w += BS) {
+            const uint32_t s0 = 2 * w, s1 = s0 + 1, g = gd[w];
+            const uint32_t d0 = 8 * (g & 0xFFFFu) - cnt[s0];
+            const uint32_t d1 = s1 < pl.nseg ? 8 * (g >> 16) - cnt[s1] : 0u;
+            gd[w] = d0 | (d1 << 16);
+        }
+    } else if constexpr (C16) {
+        block_exclusive_scan16(cnt, pl.nseg, wsum);
+    } else {
+        block_exclusive_scan<false, SPER>(cnt, pl.nseg, wsum);
+    }
     // the groups' nibble words start clear (ORed into below); the image held perm / staged keys
     // until the hashing rounds ended
     for (uint32_t g = tid; g < pl.CP / 8; g += BS) smem[g * kGroupWords + 4] = 0;
@@ -339,7 +366,8 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
             static_assert(KK > 0, "the group pack runs compiled k");
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                if (val[q] != kSentinel) posv[((uint64_t)tile * kNsMax + t + q) * BS + tid] = (uint16_t)pos[q];
+                if (val[q] != kSentinel)
+                    posv[((uint64_t)tile * kNsMax + t + q) * BS + tid] = (uint16_t)(pos[q] + gd_get(val[q] >> SB));
         }
     }
     __syncthreads();
@@ -347,6 +375,49 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     // the tile's end are whatever LDS held: every reader masks entries by the run bounds.
     const uint32_t total = seg_get<C16>(cnt, pl.nseg - 1);
     uint32_t* out = tiles + (uint64_t)tile * pl.tile_words;
+    if constexpr (POS) {
+        // gd: shifts -> each run's first group in HBM, gstart(s) = (start(s) + dlt(s)) / 8
+        for (uint32_t w = tid; w < (pl.nseg + 1) / 2; w += BS) {
+            const uint32_t s0 = 2 * w, s1 = s0 + 1, g = gd[w];
+            const uint32_t g0 = ((s0 ? cnt[s0 - 1] : 0u) + (g & 0xFFFFu)) >> 3;
+            const uint32_t g1 = s1 < pl.nseg ? (cnt[s0] + (g >> 16)) >> 3 : 0u;
+            gd[w] = g0 | (g1 << 16);
+        }
+        __syncthreads();
+        auto gend = [&](uint32_t sg) {  // one past segment sg's last group
+            const uint32_t st = sg ? cnt[sg - 1] : 0u;
+            return gd_get(sg) + ((cnt[sg] - st + 7) >> 3);
+        };
+        const uint32_t ng = gend(pl.nseg - 1);
+        // output group og: its segment (the last one starting at or before og: empty segments
+        // share their start with the next), then its 8 entries (padding past the run: zeros)
+        for (uint32_t og = tid; og < ng; og += BS) {
+            uint32_t lo_s = 0, hi_s = pl.nseg - 1;
+            while (lo_s < hi_s) {
+                const uint32_t mid = (lo_s + hi_s + 1) >> 1;
+                if (gd_get(mid) <= og) lo_s = mid;
+                else hi_s = mid - 1;
+            }
+            const uint32_t sg = lo_s, st = sg ? cnt[sg - 1] : 0u, en = cnt[sg];
+            const uint32_t e0 = st + 8 * (og - gd_get(sg));
+            uint32_t w4[4] = {0, 0, 0, 0}, nb = 0;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t e = e0 + c;
+                if (e < en) {
+                    const uint32_t l16 = lo[(e >> 3) * 10 + (e & 7)];
+                    const uint32_t n4 = (smem[(e >> 3) * kGroupWords + 4] >> (4 * (e & 7))) & 15u;
+                    w4[c >> 1] |= l16 << ((c & 1) * 16);
+                    nb |= n4 << (4 * c);
+                }
+            }
+            __builtin_memcpy(out + og * kGroupWords, w4, 16);
+            out[og * kGroupWords + 4] = nb;
+        }
+        // run ends in padded entries (multiples of 8)
+        for (uint32_t sg = tid; sg < pl.nseg; sg += BS) ends[(uint64_t)sg * pl.ntS + tile] = (uint16_t)(8 * gend(sg));
+        return;
+    }
     const uint32_t words = group_words(total);
     for (uint32_t w = tid * 4; w < words; w += BS * 4) {
         if (w + 4 <= words)
