@@ -369,8 +369,8 @@ __global__ __launch_bounds__(kPBlock) void k_group_seg2(const uint32_t* tiles, c
 // GP4: dynamic LDS = the tile's result bytes (pl.CPg, a multiple of 8).  K compile-time: a lane
 // issues the K position loads of each of its KPT keys together (one memory latency, not K * KPT).
 template <int K, int KPT>
-__global__ __launch_bounds__(kPBlock) void k_group_out2(const uint8_t* res, const uint16_t* posv, const uint16_t* endsT,
-                                                        PartPlan pl, uint32_t slots, DevKeys dk, MultiGroup g,
+__global__ __launch_bounds__(kPBlock) void k_group_out2(const uint8_t* res, const uint32_t* posv, const uint16_t* endsT,
+                                                        PartPlan pl, uint32_t pairs, DevKeys dk, MultiGroup g,
                                                         const uint8_t* bounds, uint8_t* out, uint32_t out_stride) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rl32[];
     const uint8_t* rl = reinterpret_cast<const uint8_t*>(rl32);
@@ -382,25 +382,40 @@ __global__ __launch_bounds__(kPBlock) void k_group_out2(const uint8_t* res, cons
     for (uint32_t w = tid; w * 8 < total; w += kPBlock) reinterpret_cast<uint2*>(rl32)[w] = src[w];
     __syncthreads();
     const uint32_t full = g.G >= 8 ? 0xFFu : ((1u << g.G) - 1u);
-    const uint16_t* pt = posv + (uint64_t)tile * slots * 512;
+    const uint32_t* pt = posv + (uint64_t)tile * pairs * 512;
     bool packed = g.G == 8 && (out_stride & 7u) == 0 && (g.col[0] & 7u) == 0 && !bounds &&
                   (reinterpret_cast<uintptr_t>(out) & 7u) == 0;
     for (uint32_t q = 1; q < g.G && packed; ++q) packed = g.col[q] == g.col[0] + q;
-    uint16_t p[KPT][K];
+    // key l: stash round r = l / 512, lane l % 512; its slots r*K .. r*K+K-1 sit in the u16 pairs
+    // (r*K)/2 ..; for odd K a round starts on the pair's high half when r is odd (wave-uniform:
+    // a wave's 64 keys share r)
+    constexpr int NW = K / 2 + 1;
+    uint32_t wv[KPT][NW];
 #pragma unroll
     for (int x = 0; x < KPT; ++x) {
         const uint32_t l = tid + x * kPBlock;
-        const uint32_t r = l >> 9, ln = l & 511u;  // stash round and lane of key l (512-thread pack)
+        const uint32_t r = l >> 9, ln = l & 511u;
+        const uint32_t wb = (r * K) >> 1;
 #pragma unroll
-        for (int i = 0; i < K; ++i) p[x][i] = l < nk ? pt[(r * K + i) * 512 + ln] : (uint16_t)0;
+        for (int j = 0; j < NW; ++j) wv[x][j] = (l < nk && wb + j < pairs) ? pt[(wb + j) * 512 + ln] : 0u;
     }
+    auto pos_of = [&](int x, int i, uint32_t odd) -> uint32_t {
+        const uint32_t q = odd + (uint32_t)i;
+        return (wv[x][q >> 1] >> ((q & 1u) * 16)) & 0xFFFFu;
+    };
 #pragma unroll
     for (int x = 0; x < KPT; ++x) {
         const uint32_t l = tid + x * kPBlock;
         if (l >= nk) break;
         uint32_t mk = full;
+        const uint32_t odd = ((l >> 9) * K) & 1u;
+        if (odd) {
 #pragma unroll
-        for (int i = 0; i < K; ++i) mk &= rl[p[x][i]];
+            for (int i = 0; i < K; ++i) mk &= rl[pos_of(x, i, 1u)];
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) mk &= rl[pos_of(x, i, 0u)];
+        }
         const uint64_t j = key0 + l;
         uint8_t* row = out + j * out_stride;
         if (packed) {
@@ -462,7 +477,7 @@ static uint64_t gp_workspace_bytes(uint64_t n, uint64_t m, uint32_t k) {
         const PartPlan pl = make_group_plan((uint32_t)m, k, fixed);
         const uint64_t nt = (gp_chunk_keys(pl, n) + pl.KT - 1) / pl.KT, ntS = (nt + 7) & ~7ull;
         need = std::max<uint64_t>(need, nt * (uint64_t)pl.tile_words * 4 + ntS * pl.nseg * 2 + nt * pl.CPg +
-                                            nt * (uint64_t)group_pack_slots(k) * 512 * 2 + 4 * 256);
+                                            nt * (uint64_t)((group_pack_slots(k) + 1) / 2) * 512 * 4 + 4 * 256);
     }
     return need;
 }
@@ -493,6 +508,7 @@ static hipError_t launch_multi_probe_gp(const KeyBatch& kb, const MultiGroup& g,
     uint16_t* endsT = reinterpret_cast<uint16_t*>(base + o_ends);
     uint8_t* res = reinterpret_cast<uint8_t*>(base + o_res);
     uint16_t* posv = reinterpret_cast<uint16_t*>(base + o_pos);
+    const uint32_t pairs = (slots + 1) / 2;
     const uint64_t nwords = (g.m + 31) / 32;
     hipLaunchKernelGGL(k_interleave, dim3((unsigned)((nwords + 255) / 256)), dim3(256), 0, s, g, nwords, bytes);
     // k_group_out2's dynamic LDS: the tile's result bytes (up to 64 KiB); keys per lane: KT / 1024
@@ -520,8 +536,9 @@ static hipError_t launch_multi_probe_gp(const KeyBatch& kb, const MultiGroup& g,
                            nbytes, res);
         phase_end(kPhaseProbeSeg, s);
         phase_begin(kPhaseProbeOut, s);
-        hipLaunchKernelGGL(out2, dim3(ntiles), dim3(kPBlock), (pl.CPg + 15) & ~15u, s, res, posv, endsT, pl, slots, dk,
-                           g, bounds, out + lo * out_stride, out_stride);
+        hipLaunchKernelGGL(out2, dim3(ntiles), dim3(kPBlock), (pl.CPg + 15) & ~15u, s, res,
+                           reinterpret_cast<const uint32_t*>(posv), endsT, pl, pairs, dk, g, bounds,
+                           out + lo * out_stride, out_stride);
         phase_end(kPhaseProbeOut, s);
         err = hipGetLastError();
         if (err != hipSuccess) return err;

@@ -514,8 +514,9 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
         const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)cnt_words - 4 * (int64_t)pl.gd_words;
-        // LDS = 2.5 * CP with CP <= C + 7
-        const int64_t cmax = avail * 2 / 5 - 8;
+        // LDS = 2.5 * CP with CP <= C + 7 (the group pack: runs padded to whole groups in LDS,
+        // up to 7 more entries per segment)
+        const int64_t cmax = avail * 2 / 5 - 8 - (group ? 7 * (int64_t)pl.nseg : 0);
         const int64_t kt = std::min<int64_t>((int64_t)rmax * kpr, cmax / k);
         if (kt >= kpr || per_cu == 1) {
             pl.KT = (uint32_t)std::max<int64_t>(kt, 1);
@@ -535,7 +536,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     static const int tpad = [] { const char* e = getenv("VBF_TILE_PAD"); return e ? atoi(e) : 4; }();
     pl.tile_words += (uint32_t)std::max(0, tpad) & ~3u;
     pl.nsegS = (pl.nseg + 7) & ~7u;
-    pl.lds1 = (group_words(pl.CP) + cnt_words + 16 + kLenBuckets + pl.gd_words) * 4;
+    pl.lds1 = (group_words(group ? pl.CPg : pl.CP) + cnt_words + 16 + kLenBuckets + pl.gd_words) * 4;
     // VBF_TILE_LDS_MIN (experiments, speed only): request at least this much LDS per k_tile_pack
     // workgroup, e.g. > 80 KiB to hold one workgroup per CU
     static const int lds_min = [] { const char* e = getenv("VBF_TILE_LDS_MIN"); return e ? atoi(e) : 0; }();

@@ -334,7 +334,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     }
     // the groups' nibble words start clear (ORed into below); the image held perm / staged keys
     // until the hashing rounds ended
-    for (uint32_t g = tid; g < pl.CP / 8; g += BS) smem[g * kGroupWords + 4] = 0;
+    for (uint32_t g = tid; g < (POS ? pl.CPg : pl.CP) / 8; g += BS) smem[g * kGroupWords + 4] = 0;
     __syncthreads();
     if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
         uint32_t acc = 0;
@@ -354,6 +354,11 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
             val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
             pos[q] = val[q] != kSentinel ? seg_rank<C16, SB>(cnt0, val[q]) : 0u;
         }
+        if constexpr (POS) {  // the group pack places every run at its padded place (whole groups)
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (val[q] != kSentinel) pos[q] += gd_get(val[q] >> SB);
+        }
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (val[q] != kSentinel) {
@@ -362,12 +367,14 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
                 atomicOr(&smem[g + 4], ((val[q] >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4));
             }
         }
-        if constexpr (POS) {  // coalesced: for one stash slot the lanes write consecutive u16
+        if constexpr (POS) {  // coalesced: for a pair of stash slots the lanes write consecutive u32
             static_assert(KK > 0, "the group pack runs compiled k");
+            uint32_t* pv = reinterpret_cast<uint32_t*>(posv);
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (val[q] != kSentinel)
-                    posv[((uint64_t)tile * kNsMax + t + q) * BS + tid] = (uint16_t)(pos[q] + gd_get(val[q] >> SB));
+            for (int q = 0; q < 8; q += 2)
+                if (val[q] != kSentinel || val[q + 1] != kSentinel)
+                    pv[((uint64_t)tile * ((kNsMax + 1) / 2) + (t + q) / 2) * BS + tid] =
+                        (val[q] != kSentinel ? pos[q] : 0u) | ((val[q + 1] != kSentinel ? pos[q + 1] : 0u) << 16);
         }
     }
     __syncthreads();
@@ -376,46 +383,17 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     const uint32_t total = seg_get<C16>(cnt, pl.nseg - 1);
     uint32_t* out = tiles + (uint64_t)tile * pl.tile_words;
     if constexpr (POS) {
-        // gd: shifts -> each run's first group in HBM, gstart(s) = (start(s) + dlt(s)) / 8
-        for (uint32_t w = tid; w < (pl.nseg + 1) / 2; w += BS) {
-            const uint32_t s0 = 2 * w, s1 = s0 + 1, g = gd[w];
-            const uint32_t g0 = ((s0 ? cnt[s0 - 1] : 0u) + (g & 0xFFFFu)) >> 3;
-            const uint32_t g1 = s1 < pl.nseg ? (cnt[s0] + (g >> 16)) >> 3 : 0u;
-            gd[w] = g0 | (g1 << 16);
+        // the padded image is already in LDS: copy its whole groups; run ends in padded entries
+        // (multiples of 8): end(s) + dlt(s), rounded up to the group
+        const uint32_t pwords = group_words((total + gd_get(pl.nseg - 1) + 7) & ~7u);
+        for (uint32_t w = tid * 4; w < pwords; w += BS * 4) {
+            if (w + 4 <= pwords)
+                *reinterpret_cast<uint4*>(out + w) = *reinterpret_cast<const uint4*>(smem + w);
+            else
+                for (uint32_t x = w; x < pwords; ++x) out[x] = smem[x];
         }
-        __syncthreads();
-        auto gend = [&](uint32_t sg) {  // one past segment sg's last group
-            const uint32_t st = sg ? cnt[sg - 1] : 0u;
-            return gd_get(sg) + ((cnt[sg] - st + 7) >> 3);
-        };
-        const uint32_t ng = gend(pl.nseg - 1);
-        // output group og: its segment (the last one starting at or before og: empty segments
-        // share their start with the next), then its 8 entries (padding past the run: zeros)
-        for (uint32_t og = tid; og < ng; og += BS) {
-            uint32_t lo_s = 0, hi_s = pl.nseg - 1;
-            while (lo_s < hi_s) {
-                const uint32_t mid = (lo_s + hi_s + 1) >> 1;
-                if (gd_get(mid) <= og) lo_s = mid;
-                else hi_s = mid - 1;
-            }
-            const uint32_t sg = lo_s, st = sg ? cnt[sg - 1] : 0u, en = cnt[sg];
-            const uint32_t e0 = st + 8 * (og - gd_get(sg));
-            uint32_t w4[4] = {0, 0, 0, 0}, nb = 0;
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const uint32_t e = e0 + c;
-                if (e < en) {
-                    const uint32_t l16 = lo[(e >> 3) * 10 + (e & 7)];
-                    const uint32_t n4 = (smem[(e >> 3) * kGroupWords + 4] >> (4 * (e & 7))) & 15u;
-                    w4[c >> 1] |= l16 << ((c & 1) * 16);
-                    nb |= n4 << (4 * c);
-                }
-            }
-            __builtin_memcpy(out + og * kGroupWords, w4, 16);
-            out[og * kGroupWords + 4] = nb;
-        }
-        // run ends in padded entries (multiples of 8)
-        for (uint32_t sg = tid; sg < pl.nseg; sg += BS) ends[(uint64_t)sg * pl.ntS + tile] = (uint16_t)(8 * gend(sg));
+        for (uint32_t sg = tid; sg < pl.nseg; sg += BS)
+            ends[(uint64_t)sg * pl.ntS + tile] = (uint16_t)((cnt[sg] + gd_get(sg) + 7) & ~7u);
         return;
     }
     const uint32_t words = group_words(total);
@@ -436,7 +414,8 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
 // The multi-SST group pack (vbf_partition.hip, used by vbf_multi_part.hip): k_tile_pack over
 // 2^17-position segments of an interleaved group (k = 10 or 19, keys hashed with the length prefix,
 // m <= 2^28 positions), writing the tile images, endsT[seg][tile] (row stride pl.ntS, set by the
-// caller) and every entry's place posv[tile][slot][lane] (group_pack_slots(k) slots of 512 lanes).
+// caller) and every entry's padded place in posv: u16 pairs, posv32[tile][slot / 2][lane] (slot =
+// round * k + seed; (group_pack_slots(k) + 1) / 2 pairs of 512 lanes per tile).
 bool group_pack_supported(uint64_t m, uint32_t k);
 PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed);
 uint32_t group_pack_slots(uint32_t k);
