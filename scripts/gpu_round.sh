@@ -45,6 +45,8 @@ for s in $STEPS; do
     compact) run bench_compact 600 python bench.py --compact --steps 5 --warmup 1 ;;
     multi)  run bench_multi 600 python bench.py --multi --steps 5 --warmup 1 ;;
     profmultigp) (cd /tmp && run profmultigp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmultigp" -o run -- python3 "$ROOT/bench.py" --multi --steps 10 --warmup 2) || exit $? ;;
+    probetest) run pytest_probe 900 python -u -m pytest tests/test_gpu_probe.py tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
+    abprobegp) for v in 0 1 0 1; do run probe_phases_gp$v 300 env VBF_PROBE_GP=$v python tools/probe_phases.py; done ;;
     multitest) run pytest_multi 600 python -u -m pytest tests/test_gpu_multi.py -x -v -m gpu --timeout 300 --timeout-method thread ;;
     abmultigp) for v in 0 1 0 1; do run bench_multi_gp$v 300 env VBF_MULTI_GP=$v python bench.py --multi --steps 10 --warmup 2; grep -o '"ms_per_step": [0-9.]*\|"phases".*' "$OUT/bench_multi_gp$v.log"; done ;;
     e2e)    run bench_e2e 600 python bench.py --e2e --steps 5 --warmup 1 ;;

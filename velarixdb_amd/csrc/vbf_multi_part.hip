@@ -527,7 +527,7 @@ static hipError_t launch_multi_probe_gp(const KeyBatch& kb, const MultiGroup& g,
         const uint32_t ntiles = (uint32_t)((cn + pl.KT - 1) / pl.KT);
         pl.ntS = (ntiles + 7) & ~7u;
         phase_begin(kPhaseProbePack, s);
-        hipError_t err = launch_group_pack(kb, dk, pl, ntiles, tiles, endsT, posv, s);
+        hipError_t err = launch_group_pack(kb, dk, pl, ntiles, tiles, endsT, posv, kByteSegBits, s);
         if (err != hipSuccess) return err;
         phase_end(kPhaseProbePack, s);
         phase_begin(kPhaseProbeSeg, s);

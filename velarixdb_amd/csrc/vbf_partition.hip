@@ -462,11 +462,13 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
 // fixed: the batch has a compile-time key length (pick_fmt > 0), which allows more stash rounds
 // for some k (build_rounds_max).
 // lp: the batch hashes the length prefix (Hash for [u8]; only such batches take the runtime-k
-// class kernels).  group: the multi-SST group pack (vbf_multi_part.hip) -- segments of 2^17
-// positions (bytes of 8 interleaved filters), the 512-thread shape, keys in key order.
-static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = true, bool group = false) {
+// class kernels).  group_sb != 0: the position-table pack of the probes (vbf_multi_part.hip:
+// segments of 2^17 bytes of 8 interleaved filters; vbf_probe_part.hip: 2^20 filter bits) -- the
+// 512-thread shape, keys in key order, runs padded to whole groups.
+static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = true, int group_sb = 0) {
     PartPlan pl{};
-    const int sb = group ? kByteSegBits : kSegBits;
+    const bool group = group_sb != 0;
+    const int sb = group ? group_sb : kSegBits;
     pl.k = k;
     pl.m = m;
     pl.mu = ~0ull / m;
@@ -606,17 +608,17 @@ bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k) {
     return true;
 }
 
-// ---- the multi-SST group pack (vbf_multi_part.hip): K1 with 2^17-position segments ----
-bool group_pack_supported(uint64_t m, uint32_t k) {
-    if (m == 0 || m > (1ull << 28) || (k != 10 && k != 19)) return false;  // <= 2 048 segments
+// ---- the position-table pack of the probes: K1 with 2^sb-position segments ----
+bool group_pack_supported(uint64_t m, uint32_t k, int sb) {
+    if (m == 0 || m > (2048ull << sb) || m > (1ull << 31) || (k != 10 && k != 19)) return false;  // <= 2 048 segments
     for (bool fixed : {true, false}) {
-        const PartPlan pl = make_plan((uint32_t)m, k, fixed, true, true);
+        const PartPlan pl = make_plan((uint32_t)m, k, fixed, true, sb);
         if (pl.lds1 > kLdsPerCu / 2 || pl.CPg > 65535 || pl.nseg > 4 * 512) return false;
     }
     return true;
 }
 
-PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed) { return make_plan(m, k, fixed, true, true); }
+PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed, int sb) { return make_plan(m, k, fixed, true, sb); }
 
 uint32_t group_pack_slots(uint32_t k) {
     const K1Shape sh = k1_shape((int)k, true, 1);
@@ -624,13 +626,17 @@ uint32_t group_pack_slots(uint32_t k) {
 }
 
 hipError_t launch_group_pack(const KeyBatch& kb, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
-                             uint32_t* tiles, uint16_t* endsT, uint16_t* posv, hipStream_t s) {
+                             uint32_t* tiles, uint16_t* endsT, uint16_t* posv, int sb, hipStream_t s) {
     hipError_t err = hipErrorInvalidValue;
     if (!kb.len_prefix || (pl.k != 10 && pl.k != 19) || pl.k1v != 1 || !pl.ends_t) return err;
+    if (sb != kByteSegBits && sb != kSegBits) return err;
     with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), true, [&]<int FMT, bool LP>() {
         if constexpr (LP) {
-            auto fn = pl.k == 10 ? k_tile_pack<FMT, true, 10, true, false, 1, 0, kByteSegBits, true>
-                                 : k_tile_pack<FMT, true, 19, true, false, 1, 0, kByteSegBits, true>;
+            auto fn = sb == kByteSegBits
+                          ? (pl.k == 10 ? k_tile_pack<FMT, true, 10, true, false, 1, 0, kByteSegBits, true>
+                                        : k_tile_pack<FMT, true, 19, true, false, 1, 0, kByteSegBits, true>)
+                          : (pl.k == 10 ? k_tile_pack<FMT, true, 10, true, false, 1, 0, kSegBits, true>
+                                        : k_tile_pack<FMT, true, 19, true, false, 1, 0, kSegBits, true>);
             hipFuncAttributes fa{};
             err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
             if (err == hipSuccess && fa.sharedSizeBytes != 0) err = hipErrorInvalidKernelFile;

@@ -1,6 +1,6 @@
 // vbf_probe_part.hip -- the partitioned probe (contains() for large batches): the build's
 // tile/segment scheme (vbf_partition.hip) applied to lookups.
-#include "vbf_partition.hpp"
+#include "vbf_tile_pack.hpp"
 
 namespace vbf {
 
@@ -305,6 +305,271 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out(const uint32_t* tiles, co
     }
 }
 
+// ---- Round 4: the partitioned probe on the build's image (k = 10 / 19 with the length prefix,
+// m <= 2^31; VBF_PROBE_GP = 0 keeps the pipeline above) ----
+// PP1 launch_group_pack(sb = 20): k_tile_pack writing the 2.5-byte 8-entry group image with every
+// run padded to whole groups, the padded run ends transposed, and every entry's padded place in
+// posv (u16 pairs per stash slot pair and lane).
+// PP3 k_probe_seg2: k_seg_or's flattened reader over a segment's runs (whole groups): a group's 8
+// filter bits -> one result byte at res[tile][group] (no run shares a group, so one plain store).
+// PP4 k_probe_out2: the tile's result bits staged in LDS, each key's k bits found through posv and
+// ANDed: the answer byte, or the tile's hit count.
+template <int NG = 4>
+__global__ __launch_bounds__(kPBlock) void k_probe_seg2(const uint32_t* tiles, const uint16_t* endsT, uint32_t ntiles,
+                                                        PartPlan pl, uint32_t G, const uint32_t* words, uint8_t* res) {
+    __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
+    const uint32_t nwg = gridDim.x, qq = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+    const uint32_t wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + blockIdx.x / 8;
+    const uint32_t seg = wg / G, part = wg % G;
+    const uint32_t t_lo = (uint32_t)((uint64_t)part * ntiles / G), t_hi = (uint32_t)((uint64_t)(part + 1) * ntiles / G);
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t wbase = (uint64_t)seg * kSegWords;
+    const uint32_t wn = (uint32_t)std::min<uint64_t>(kSegWords, pl.nwords - wbase);
+    for (uint32_t w = tid * 4; w < kSegWords; w += kPBlock * 4) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (w + 4 <= wn) {
+            v = *reinterpret_cast<const uint4*>(words + wbase + w);
+        } else if (w < wn) {
+            v.x = words[wbase + w];
+            if (w + 1 < wn) v.y = words[wbase + w + 1];
+            if (w + 2 < wn) v.z = words[wbase + w + 2];
+        }
+        *reinterpret_cast<uint4*>(bitmap + w) = v;
+    }
+    __syncthreads();
+    const uint16_t* row_end = endsT + (uint64_t)seg * pl.ntS;
+    const uint16_t* row_beg = seg ? endsT + (uint64_t)(seg - 1) * pl.ntS : nullptr;
+    const uint32_t rstride = pl.CPg / 8;  // result bytes per tile
+    auto lb = [&](uint32_t t0) -> uint32_t {
+        const uint32_t t = t0 + lane;
+        uint32_t v = 0;
+        if (t < t_hi) v = (row_beg ? (uint32_t)row_beg[t] : 0u) | ((uint32_t)row_end[t] << 16);
+        return v;
+    };
+    auto answer = [&](uint32_t t, uint32_t gi, uint4 l, uint32_t nib) {
+        const uint32_t w[4] = {l.x, l.y, l.z, l.w};
+        uint32_t r = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t off = ((w[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) | (((nib >> (4 * c)) & 15u) << 16);
+            r |= ((bitmap[off >> 5] >> (off & 31)) & 1u) << c;
+        }
+        res[(uint64_t)t * rstride + gi] = (uint8_t)r;
+    };
+    const uint32_t wstep = (kPBlock / 64) * 64;
+    struct FB {
+        uint32_t v, excl, total;
+        uint4 l[NG];
+        uint32_t nib[NG], ok[NG], t[NG], gi[NG];
+    };
+    auto prep = [&](uint32_t v, FB& b) {  // padded runs: whole groups
+        const uint32_t ch = ((v >> 16) - (v & 0xFFFFu)) >> 3;
+        uint32_t incl = ch;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= (uint32_t)o) incl += y;
+        }
+        b.v = v;
+        b.excl = incl - ch;
+        b.total = (uint32_t)__shfl((int)incl, 63);
+    };
+    auto locate = [&](const FB& b, uint32_t t0, uint32_t c, uint32_t& t, uint32_t& gi) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int sft = 32; sft; sft >>= 1)
+            if ((uint32_t)__shfl((int)b.excl, (int)r + sft) <= c) r += sft;
+        const uint32_t rv = (uint32_t)__shfl((int)b.v, (int)r), rex = (uint32_t)__shfl((int)b.excl, (int)r);
+        t = std::min(t0 + r, t_hi - 1);
+        gi = ((rv & 0xFFFFu) >> 3) + (c - rex);
+        return c < b.total ? 1u : 0u;
+    };
+    auto issue = [&](uint32_t t0, FB& b) {
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            b.ok[q] = locate(b, t0, (uint32_t)q * 64 + lane, b.t[q], b.gi[q]);
+            if (b.ok[q]) {
+                const uint32_t* tile = tiles + (uint64_t)b.t[q] * pl.tile_words;
+                __builtin_memcpy(&b.l[q], tile + b.gi[q] * 5, 16);
+                b.nib[q] = tile[b.gi[q] * 5 + 4];
+            }
+        }
+    };
+    auto consume = [&](uint32_t t0, const FB& b) {
+#pragma unroll
+        for (int q = 0; q < NG; ++q)
+            if (b.ok[q]) answer(b.t[q], b.gi[q], b.l[q], b.nib[q]);
+#pragma unroll 1
+        for (uint32_t c0 = 64 * NG; c0 < b.total; c0 += 64) {
+            uint32_t t, gi;
+            if (locate(b, t0, c0 + lane, t, gi)) {
+                const uint32_t* tile = tiles + (uint64_t)t * pl.tile_words;
+                uint4 l;
+                __builtin_memcpy(&l, tile + gi * 5, 16);
+                answer(t, gi, l, tile[gi * 5 + 4]);
+            }
+        }
+    };
+    uint32_t t0 = t_lo + wave * 64;
+    FB A, B;
+    uint32_t v1 = lb(t0 + wstep);
+    prep(lb(t0), A);
+    if (t0 < t_hi) issue(t0, A);
+    while (t0 < t_hi) {
+        prep(v1, B);
+        uint32_t v2 = lb(t0 + 2 * wstep);
+        const bool more = t0 + wstep < t_hi;
+        if (more) issue(t0 + wstep, B);
+        consume(t0, A);
+        t0 += wstep;
+        if (!more) break;
+        prep(v2, A);
+        v1 = lb(t0 + 2 * wstep);
+        const bool more2 = t0 + wstep < t_hi;
+        if (more2) issue(t0 + wstep, A);
+        consume(t0, B);
+        t0 += wstep;
+        if (!more2) break;
+    }
+}
+
+// PP4 (OUT 0: answer bytes, 1: hits of the tile -> partial[tile]).  K compile-time: a lane issues the
+// position loads of its KPT keys together.
+template <int K, int KPT, int OUT>
+__global__ __launch_bounds__(kPBlock) void k_probe_out2(const uint8_t* res, const uint32_t* posv, PartPlan pl,
+                                                        uint32_t pairs, uint64_t n, uint8_t* out, uint32_t* partial) {
+    __shared__ uint32_t rl32[65536 / 8 / 4];  // the tile's result bits (<= CPg / 8 bytes)
+    __shared__ uint32_t wsum[kPBlock / 64];
+    const uint8_t* rl = reinterpret_cast<const uint8_t*>(rl32);
+    const uint32_t tid = threadIdx.x, tile = blockIdx.x;
+    const uint64_t key0 = (uint64_t)tile * pl.KT;
+    const uint32_t nk = (uint32_t)std::min<uint64_t>(pl.KT, n - key0);
+    const uint32_t rbytes = pl.CPg / 8;
+    const uint8_t* src = res + (uint64_t)tile * rbytes;
+    for (uint32_t b = tid; b < rbytes; b += kPBlock) reinterpret_cast<uint8_t*>(rl32)[b] = src[b];
+    __syncthreads();
+    const uint32_t* pt = posv + (uint64_t)tile * pairs * 512;
+    constexpr int NW = K / 2 + 1;
+    uint32_t wv[KPT][NW];
+#pragma unroll
+    for (int x = 0; x < KPT; ++x) {
+        const uint32_t l = tid + x * kPBlock;
+        const uint32_t r = l >> 9, ln = l & 511u;
+        const uint32_t wb = (r * K) >> 1;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) wv[x][j] = (l < nk && wb + j < pairs) ? pt[(wb + j) * 512 + ln] : 0u;
+    }
+    auto bit_at = [&](int x, int i, uint32_t odd) -> uint32_t {
+        const uint32_t q = odd + (uint32_t)i;
+        const uint32_t p = (wv[x][q >> 1] >> ((q & 1u) * 16)) & 0xFFFFu;
+        return (rl[p >> 3] >> (p & 7)) & 1u;
+    };
+    uint32_t hits = 0;
+#pragma unroll
+    for (int x = 0; x < KPT; ++x) {
+        const uint32_t l = tid + x * kPBlock;
+        if (l >= nk) break;
+        uint32_t ok = 1;
+        const uint32_t odd = ((l >> 9) * K) & 1u;
+        if (odd) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) ok &= bit_at(x, i, 1u);
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) ok &= bit_at(x, i, 0u);
+        }
+        if constexpr (OUT == 0) out[key0 + l] = (uint8_t)ok;
+        else hits += ok;
+    }
+    if constexpr (OUT == 1) {
+        for (int o = 32; o > 0; o >>= 1) hits += __shfl_down(hits, o);
+        if ((tid & 63) == 0) wsum[tid >> 6] = hits;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < kPBlock / 64; ++w) t += wsum[w];
+            partial[blockIdx.x] = t;
+        }
+    }
+}
+
+static bool pp_enabled(uint32_t m, uint32_t k, bool lp) {
+    const char* e = getenv("VBF_PROBE_GP");  // read per call (A/B)
+    return (e ? atoi(e) : 1) != 0 && lp && group_pack_supported(m, k, kSegBits);
+}
+
+static uint64_t pp_chunk_keys(const PartPlan& pl, uint64_t n) {
+    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, kPartChunkIdx / pl.C);
+    return std::min<uint64_t>(n, tiles_per_chunk * pl.KT);
+}
+
+// tiles, endsT[nseg][ntS], res[tiles][CPg / 8], posv (u16 pairs), partial counts
+static uint64_t pp_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
+    uint64_t need = 0;
+    for (bool fixed : {true, false}) {
+        const PartPlan pl = make_group_plan(m, k, fixed, kSegBits);
+        const uint64_t nt = (pp_chunk_keys(pl, n) + pl.KT - 1) / pl.KT, ntS = (nt + 7) & ~7ull;
+        need = std::max<uint64_t>(need, nt * (uint64_t)pl.tile_words * 4 + ntS * pl.nseg * 2 + nt * (pl.CPg / 8) +
+                                            nt * (uint64_t)((group_pack_slots(k) + 1) / 2) * 512 * 4 + nt * 4 +
+                                            5 * 256);
+    }
+    return need;
+}
+
+static hipError_t launch_probe_pp(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                                  unsigned long long* count, void* ws, hipStream_t s) {
+    auto align256 = [](uint64_t x) { return (x + 255) & ~255ull; };
+    PartPlan pl = make_group_plan(m, k, pick_fmt(kb.keys, kb.offsets, kb.stride) > 0, kSegBits);
+    const uint32_t pairs = (group_pack_slots(k) + 1) / 2;
+    const uint64_t chunk_keys = pp_chunk_keys(pl, kb.n);
+    const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT, max_ntS = (max_tiles + 7) & ~7ull;
+    char* base = static_cast<char*>(ws);
+    const uint64_t o_ends = align256(max_tiles * pl.tile_words * 4);
+    const uint64_t o_res = align256(o_ends + max_ntS * pl.nseg * 2);
+    const uint64_t o_pos = align256(o_res + max_tiles * (pl.CPg / 8));
+    const uint64_t o_part = align256(o_pos + max_tiles * pairs * 512 * 4);
+    uint32_t* tiles = reinterpret_cast<uint32_t*>(base);
+    uint16_t* endsT = reinterpret_cast<uint16_t*>(base + o_ends);
+    uint8_t* res = reinterpret_cast<uint8_t*>(base + o_res);
+    uint32_t* posv = reinterpret_cast<uint32_t*>(base + o_pos);
+    uint32_t* partial = reinterpret_cast<uint32_t*>(base + o_part);
+    const bool k10 = k == 10;
+    if (pl.KT > 1024u * (k10 ? 3u : 2u) || pl.CPg / 8 > 65536 / 8) return hipErrorInvalidValue;
+    for (uint64_t lo = 0; lo < kb.n; lo += chunk_keys) {
+        const uint64_t cn = std::min<uint64_t>(chunk_keys, kb.n - lo);
+        DevKeys dk{kb.keys, kb.offsets, kb.off_base, kb.stride, cn};
+        if (kb.offsets)
+            dk.offsets = kb.offsets + lo;
+        else
+            dk.keys = kb.keys + lo * kb.stride;
+        const uint32_t ntiles = (uint32_t)((cn + pl.KT - 1) / pl.KT);
+        pl.ntS = (ntiles + 7) & ~7u;
+        phase_begin(kPhaseProbePack, s);
+        hipError_t err = launch_group_pack(kb, dk, pl, ntiles, tiles, endsT, reinterpret_cast<uint16_t*>(posv), kSegBits, s);
+        if (err != hipSuccess) return err;
+        phase_end(kPhaseProbePack, s);
+        phase_begin(kPhaseProbeSeg, s);
+        const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
+        hipLaunchKernelGGL(k_probe_seg2<4>, dim3(pl.nseg * G), dim3(kPBlock), 0, s, tiles, endsT, ntiles, pl, G, words,
+                           res);
+        phase_end(kPhaseProbeSeg, s);
+        phase_begin(kPhaseProbeOut, s);
+        if (count) {
+            auto fn = k10 ? k_probe_out2<10, 3, 1> : k_probe_out2<19, 2, 1>;
+            hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, pairs, cn, nullptr, partial);
+            err = launch_count_finish(partial, ntiles, count, s);
+            if (err != hipSuccess) return err;
+        } else {
+            auto fn = k10 ? k_probe_out2<10, 3, 0> : k_probe_out2<19, 2, 0>;
+            hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, pairs, cn, out + lo, nullptr);
+        }
+        phase_end(kPhaseProbeOut, s);
+        err = hipGetLastError();
+        if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
+}
+
 ProbePlan make_probe_plan(uint32_t m, uint32_t k, int sb) {
     ProbePlan pl{};
     pl.k = k;
@@ -339,7 +604,9 @@ uint64_t probe_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     if (!probe_partition_supported(m, k)) return 0;
     const ProbePlan pl = make_probe_plan(m, k, kSegBits);
     const uint64_t ntiles = (probe_chunk_keys(pl, n) + pl.KT - 1) / pl.KT;
-    return ntiles * ((uint64_t)pl.cap * 4 + pl.cap / 8 + (uint64_t)pl.nseg * 4 + 4) + 1024;
+    uint64_t need = ntiles * ((uint64_t)pl.cap * 4 + pl.cap / 8 + (uint64_t)pl.nseg * 4 + 4) + 1024;
+    if (group_pack_supported(m, k, kSegBits)) need = std::max<uint64_t>(need, pp_workspace_bytes(n, m, k));
+    return need;
 }
 
 uint64_t probe_count_partials(uint64_t n, uint32_t m, uint32_t k) {
@@ -384,6 +651,7 @@ hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
     const uint64_t chunk_keys = probe_chunk_keys(pl, kb.n);
     const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
     if (ws_bytes < probe_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;
+    if (pp_enabled(m, k, kb.len_prefix)) return launch_probe_pp(kb, m, k, words, out, count, ws, s);
     auto align16 = [](uint64_t x) { return (x + 15) & ~15ull; };
     char* base = static_cast<char*>(ws);
     uint32_t* tiles = reinterpret_cast<uint32_t*>(base);

@@ -416,10 +416,12 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
 // m <= 2^28 positions), writing the tile images, endsT[seg][tile] (row stride pl.ntS, set by the
 // caller) and every entry's padded place in posv: u16 pairs, posv32[tile][slot / 2][lane] (slot =
 // round * k + seed; (group_pack_slots(k) + 1) / 2 pairs of 512 lanes per tile).
-bool group_pack_supported(uint64_t m, uint32_t k);
-PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed);
+// The same over 2^20-bit segments of one filter (sb = kSegBits) serves the single-filter
+// partitioned probe (vbf_probe_part.hip).
+bool group_pack_supported(uint64_t m, uint32_t k, int sb = kByteSegBits);
+PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed, int sb = kByteSegBits);
 uint32_t group_pack_slots(uint32_t k);
 hipError_t launch_group_pack(const KeyBatch& kb, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
-                             uint32_t* tiles, uint16_t* endsT, uint16_t* posv, hipStream_t s);
+                             uint32_t* tiles, uint16_t* endsT, uint16_t* posv, int sb, hipStream_t s);
 
 }  // namespace vbf
