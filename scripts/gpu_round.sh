@@ -93,6 +93,7 @@ for s in $STEPS; do
     abc16)  run ab_c16 900 env AB_PARITY=1 AB_ENVS="VBF_C16=1 VBF_C16=0" bash tools/env_ab.sh ;;
     abc16_19) run ab_c16_19 600 env AB_ENVS="VBF_C16=0 VBF_C16=1 VBF_C16=0 VBF_C16=1" AB_ARGS="--bits-per-key 19" bash tools/env_ab.sh ;;
     abc16_5) run ab_c16_5 600 bash -c 'for e in 0 1 0 1; do VBF_C16=$e python bench.py --config 5 --keys 250000000 --steps 5 --warmup 1 --no-cpu-baseline --neg-keys 1000000 | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(\"C16=$e\", round(d[\"ms_per_step\"],3), \"ms\", round(d[\"build_kernel_ms\"],3))"; done' ;;
+    prof19f) (cd /tmp && run prof19 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof19" -o run -- python3 "$ROOT/bench.py" --bits-per-key 19 --steps 40 --warmup 5 --no-cpu-baseline) || exit $? ;;
     prof)   (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOT/bench.py" --steps 40 --warmup 5 --no-cpu-baseline) || exit $? ;;
   esac
 done
