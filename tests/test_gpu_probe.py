@@ -91,3 +91,43 @@ def test_partitioned_probe_edges(vbf):
     assert bool(o.all())
     with pytest.raises(VbfError):
         call("vbf_probe_dev_ex", P(keys), None, 16, 100, 1, m, 33, P(words), P(o), 2, None)
+
+
+@pytest.mark.parametrize("L,m,k,n", [(16, 5_000, 10, 300_000), (None, 2_000_003, 19, 400_000),
+                                     (32, 1 << 31, 19, 300_000), (8, 70_000_000, 10, 1_200_000)])
+def test_position_table_probe_matches_round3_pipeline(vbf, ora, L, m, k, n):
+    """The round-4 partitioned probe (VBF_PROBE_GP=1: the build's image, runs padded to whole
+    groups, a position table) against the round-3 pipeline (VBF_PROBE_GP=0), answers and counts,
+    and the oracle on a slice: one segment (m = 5 000, every tile split over many workgroups),
+    variable-length keys at k = 19, the largest m of the path (2^31: 2 048 segments)."""
+    import os
+    import torch
+    from velarixdb_amd._lib import call
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    keys, offs, stride = _keys(torch, L, n, 0x5EED0131)
+    words = torch.zeros((m + 31) // 32, dtype=torch.int32, device="cuda:0")
+    half = n // 2
+    call("vbf_build_dev_ex", P(keys), P(offs), stride, half, 1, m, k, P(words), 0, None)
+    res = {}
+    for gp in ("1", "0"):
+        os.environ["VBF_PROBE_GP"] = gp
+        try:
+            o = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+            call("vbf_probe_dev_ex", P(keys), P(offs), stride, n, 1, m, k, P(words), P(o), 2, None)
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+            call("vbf_probe_count_dev_ex", P(keys), P(offs), stride, n, 1, m, k, P(words), P(cnt), 2, None)
+            torch.cuda.synchronize()
+            res[gp] = (o.cpu().numpy(), int(cnt.item()))
+        finally:
+            os.environ.pop("VBF_PROBE_GP", None)
+    assert np.array_equal(res["1"][0], res["0"][0]) and res["1"][1] == res["0"][1] == int(res["1"][0].sum())
+    assert res["1"][0][:half].all()
+    sl = slice(half - 500, min(n, half + 20000))
+    if offs is None:
+        batch = vbf.pack_fixed(keys.cpu().numpy().reshape(n, L)[sl], 1)
+    else:
+        o_h = offs.cpu().numpy().view(np.uint64)
+        kb = keys.cpu().numpy()
+        lo, hi = int(o_h[sl.start]), int(o_h[sl.stop])
+        batch = vbf.pack_offsets(kb[lo:hi], o_h[sl.start:sl.stop + 1] - lo, 1)
+    assert np.array_equal(ora.probe(batch, m, k, words.cpu().numpy().view(np.uint32)).astype(np.uint8), res["1"][0][sl])
