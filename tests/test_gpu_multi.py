@@ -256,12 +256,13 @@ def test_group_pipeline_matches_round3_pipeline_and_oracle(vbf, ora, multi_mode,
         assert np.array_equal(got[sl, s_].astype(bool), want), s_
 
 
-@pytest.mark.parametrize("m,k", [(268_434_000, 19), (5_000, 10), (40_000_003, 10)])
+@pytest.mark.parametrize("m,k", [(120_000_000, 10), (268_434_000, 19), (5_000, 10), (40_000_003, 10)])
 def test_group_pipeline_edge_sizes(vbf, ora, multi_mode, m, k):
-    """The group pipeline at its size limits: m just under 2^28 positions (2 048 segments of
-    2^17, sparse filters: short and empty runs, the padded copy-out's binary search over empty
-    segments), one segment (m = 5 000: every tile split over many workgroups), and a mid size;
-    8 filters of one (m, k), device keys; equal to the round-3 pipeline and to the oracle."""
+    """The group pipeline at its size limits: 916 segments of 2^17 with sparse filters (short and
+    empty runs), m just under 2^28 at k = 19 (2 048 segments: the run-padding reserve would take
+    most of the tile, so the round-3 pipeline answers -- the same answers either way), one segment
+    (m = 5 000: every tile split over many workgroups), and a mid size; 8 filters of one (m, k),
+    device keys; equal to the round-3 pipeline and to the oracle."""
     import torch
     from velarixdb_amd._lib import call
     from velarixdb_amd.keys import HostBatch

@@ -95,7 +95,7 @@ def test_partitioned_probe_edges(vbf):
 
 @pytest.mark.parametrize("L,m,k,n", [(16, 5_000, 10, 300_000), (None, 2_000_003, 19, 400_000),
                                      (32, 1 << 31, 19, 300_000), (8, 70_000_000, 10, 1_200_000),
-                                     (16, 1_900_000_000, 19, 60_000_000)])  # 1.14e9 entries: 2 chunks
+                                     (16, 1_200_000_000, 10, 120_000_000)])  # 1.2e9 entries: 2 chunks
 def test_position_table_probe_matches_round3_pipeline(vbf, ora, L, m, k, n):
     """The round-4 partitioned probe (VBF_PROBE_GP=1: the build's image, runs padded to whole
     groups, a position table) against the round-3 pipeline (VBF_PROBE_GP=0), answers and counts,

@@ -614,6 +614,11 @@ bool group_pack_supported(uint64_t m, uint32_t k, int sb) {
     for (bool fixed : {true, false}) {
         const PartPlan pl = make_plan((uint32_t)m, k, fixed, true, sb);
         if (pl.lds1 > kLdsPerCu / 2 || pl.CPg > 65535 || pl.nseg > 4 * 512) return false;
+        // the worst-case run padding (7 entries per segment) must leave the tile most of the LDS:
+        // at k = 19, m = 1.9e9 (1 812 segments) it would take half of it, the tile would drop to
+        // 823 keys and the segment pass would read 2.7x the runs (measured slower than the round-3
+        // probe: 15.4 vs 14.2 ms per 100M positives, profiles/r04/bench_k19.log)
+        if (7ull * pl.nseg * 20 > 9ull * pl.C) return false;
     }
     return true;
 }
