@@ -33,6 +33,11 @@ for s in $STEPS; do
     benchnostagger) run bench_nostagger 300 env VBF_STAGGER=0 python bench.py --no-cpu-baseline ;;
     benchstagger14) run bench_stagger14 300 env VBF_STAGGER=14 python bench.py --no-cpu-baseline ;;
     ablate) run ablate 300 python tools/ablate.py ;;
+    ubhash) run ubench_hash 300 ./tools/ubench hash ;;
+    abrotl) run ab_rotl 600 env AB_LIB=velarixdb_amd/libvbf_ab.so tools/ab_lib.sh 3 ;;
+    abrotl19) run ab_rotl19 600 env AB_LIB=velarixdb_amd/libvbf_ab.so tools/ab_lib.sh 3 --bits-per-key 19 ;;
+    abrotl3) run ab_rotl3 600 env AB_LIB=velarixdb_amd/libvbf_ab.so tools/ab_lib.sh 2 --config 3 --steps 5 --warmup 1 ;;
+    abparity) run pytest_ab_parity 900 env VBF_LIB=velarixdb_amd/libvbf_ab.so python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     ablatesst) run ablate_sst 300 python tools/ablate_sst.py ;;
     probephases) run probe_phases 300 python tools/probe_phases.py ;;
     benchatomic) run bench_atomic 300 python bench.py --no-cpu-baseline --strategy 1 --steps 3 ;;

@@ -31,6 +31,16 @@ __device__ __forceinline__ uint64_t rotl_a(uint64_t x) {
     return ((uint64_t)nhi << 32) | nlo;
 }
 __device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x >> 32) | (x << 32); }
+// V9: rotate as one 32-bit shift of the high word + one v_lshl_add_u64: (x << B) + (hi >> (32 - B))
+// (the two parts share no bit, so + is |)
+// (LLVM turns the disjoint + into v_lshlrev_b64 + v_or: the add is written as asm)
+template <int B>
+__device__ __forceinline__ uint64_t rotl_l(uint64_t x) {
+    const uint64_t y = (uint64_t)((uint32_t)(x >> 32) >> (32 - B));
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, %2, %3" : "=v"(r) : "v"(x), "n"(B), "v"(y));
+    return r;
+}
 // 64-bit add as add_co/addc through inline asm (defeats v_lshl_add_u64 selection)
 __device__ __forceinline__ uint64_t add_cc(uint64_t a, uint64_t b) {
     uint32_t lo, hi;
@@ -71,7 +81,12 @@ __device__ __forceinline__ uint64_t swap_pk(uint64_t x) {
 
 template <int V>
 __device__ __forceinline__ void round_(S& s) {
-    if constexpr (V == 6) {
+    if constexpr (V == 9) {
+        s.v0 += s.v1; s.v1 = rotl_l<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap32(s.v0);
+        s.v2 += s.v3; s.v3 = rotl_l<16>(s.v3); s.v3 ^= s.v2;
+        s.v0 += s.v3; s.v3 = rotl_l<21>(s.v3); s.v3 ^= s.v0;
+        s.v2 += s.v1; s.v1 = rotl_l<17>(s.v1); s.v1 ^= s.v2; s.v2 = swap32(s.v2);
+    } else if constexpr (V == 6) {
         s.v0 += s.v1; s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap_pk(s.v0);
         s.v2 += s.v3; s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
         s.v0 += s.v3; s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
@@ -183,7 +198,7 @@ __global__ __launch_bounds__(BS) void k_hash2(uint64_t n, int k, uint64_t m, uin
     extern __shared__ uint32_t pad[];
     uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
     if (j >= n) return;
-    constexpr int V = MODE == 3 ? 3 : MODE == 5 ? 5 : MODE == 6 ? 6 : MODE == 7 ? 6 : 1;
+    constexpr int V = MODE == 3 ? 3 : MODE == 5 ? 5 : MODE == 6 ? 6 : MODE == 7 ? 6 : MODE == 9 ? 9 : 1;
     S s{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL, 0x7465646279746573ULL};
     if constexpr (V == 5) s.v2 = swap32(s.v2);  // stored form
     comp<V>(s, 16); comp<V>(s, j * 0x9E3779B97F4A7C15ULL); comp<V>(s, j);
@@ -335,6 +350,17 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 64; ++i) bad += h1[i] != h5[i];
         printf("V5 == V1 hashes: %s\n", bad ? "MISMATCH" : "ok");
     }
+    {
+        uint64_t *c1, *c9;
+        CHECK(hipMalloc(&c1, 64 * 8)); CHECK(hipMalloc(&c9, 64 * 8));
+        hipLaunchKernelGGL(k_hash_check<1>, dim3(1), dim3(64), 0, 0, c1);
+        hipLaunchKernelGGL(k_hash_check<9>, dim3(1), dim3(64), 0, 0, c9);
+        uint64_t h1[64], h9[64];
+        CHECK(hipMemcpy(h1, c1, 512, hipMemcpyDeviceToHost)); CHECK(hipMemcpy(h9, c9, 512, hipMemcpyDeviceToHost));
+        int bad = 0;
+        for (int i = 0; i < 64; ++i) bad += h1[i] != h9[i];
+        printf("V9 (shift + v_lshl_add_u64 rotates) == V1 hashes: %s\n", bad ? "MISMATCH" : "ok");
+    }
     float t0 = time_ms([&] { hipLaunchKernelGGL(k_hash<0>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
     float t1 = time_ms([&] { hipLaunchKernelGGL(k_hash<1>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
     float t2 = time_ms([&] { hipLaunchKernelGGL(k_hash<2>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
@@ -351,6 +377,9 @@ int main(int argc, char** argv) {
         printf("hash variants, 100M keys x k=10 (m = 1e9):\n");
         run(k_hash2<0, 256>, 256, 0, "V1 hash only, 256 thr");
         run(k_hash2<1, 256>, 256, 0, "V1 + mod, 256 thr");
+        run(k_hash2<9, 256>, 256, 0, "V9 shift+lshl_add rotates + mod, 256 thr");
+        run(k_hash2<1, 256>, 256, 0, "V1 + mod, 256 thr (again)");
+        run(k_hash2<9, 256>, 256, 0, "V9 shift+lshl_add rotates + mod, 256 thr (again)");
         run(k_hash2<2, 256>, 256, 0, "V1 2-seed interleave + mod, 256 thr");
         run(k_hash2<3, 256>, 256, 0, "V3 addc + mod, 256 thr");
         run(k_hash2<5, 256>, 256, 0, "V5 swap-folded carry adds + mod, 256 thr");
