@@ -32,8 +32,9 @@ __device__ __forceinline__ uint64_t rotl_a(uint64_t x) {
 }
 __device__ __forceinline__ uint64_t swap32(uint64_t x) { return (x >> 32) | (x << 32); }
 // V9: rotate as one 32-bit shift of the high word + one v_lshl_add_u64: (x << B) + (hi >> (32 - B))
-// (the two parts share no bit, so + is |)
-// (LLVM turns the disjoint + into v_lshlrev_b64 + v_or: the add is written as asm)
+// (the two parts share no bit, so + is |; LLVM turns a C + into v_lshlrev_b64 + v_or, hence asm).
+// Measured round 4: WRONG (the check prints MISMATCH: the instruction's shift field is 3 bits, so a
+// shift by 13..21 is not encodable as such) and slower anyway (2.93 vs 2.85 ms) -- kept as a record.
 template <int B>
 __device__ __forceinline__ uint64_t rotl_l(uint64_t x) {
     const uint64_t y = (uint64_t)((uint32_t)(x >> 32) >> (32 - B));

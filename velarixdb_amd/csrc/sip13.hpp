@@ -15,11 +15,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-// VBF_ROTL_LA=1 (A/B build): rotates as a shift + v_lshl_add_u64 instead of two v_alignbit_b32
-#ifndef VBF_ROTL_LA
-#define VBF_ROTL_LA 0
-#endif
-
 namespace vbf {
 
 struct Sip {
@@ -32,14 +27,7 @@ struct Sip {
 // host-resident (memtable) filters runs the same rounds on the CPU (vbf_api.hip).
 template <int B>
 __host__ __device__ __forceinline__ uint64_t rotl64(uint64_t x) {
-#if defined(__HIP_DEVICE_COMPILE__) && VBF_ROTL_LA
-    // (x << B) + (hi >> (32 - B)): one full-rate shift and one v_lshl_add_u64 (the two parts share
-    // no bit, so + is |; LLVM would turn a C + into v_lshlrev_b64 + v_or, hence the asm)
-    const uint64_t y = (uint64_t)((uint32_t)(x >> 32) >> (32 - B));
-    uint64_t r;
-    asm("v_lshl_add_u64 %0, %1, %2, %3" : "=v"(r) : "v"(x), "n"(B), "v"(y));
-    return r;
-#elif defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
     const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - B);
     const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - B);
