@@ -80,9 +80,26 @@ __device__ __forceinline__ uint64_t swap_pk(uint64_t x) {
     return r;
 }
 
+// V10: swap32(a) + b as v_mad_u64_u32(a.hi, 1, b) (64-bit: carries into the high word) plus a.lo
+// added to the high word -- no v_mov pair re-aligning the swapped value
+__device__ __forceinline__ uint64_t add_swm(uint64_t a, uint64_t b) {
+    uint64_t r, c;
+    asm("v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"(r), "=s"(c) : "v"((uint32_t)(a >> 32)), "v"(b));
+    (void)c;
+    uint32_t hi;  // a 32-bit add (LLVM would fold a C add back into a 64-bit one + a v_mov)
+    asm("v_add_u32 %0, %1, %2" : "=v"(hi) : "v"((uint32_t)(r >> 32)), "v"((uint32_t)a));
+    return ((uint64_t)hi << 32) | (uint32_t)r;
+}
+
 template <int V>
 __device__ __forceinline__ void round_(S& s) {
-    if constexpr (V == 9) {
+    if constexpr (V == 10) {
+        // v0 and v2 kept un-swapped where the swap feeds an add (logical v2 = swap32(stored) at exit)
+        s.v0 += s.v1; s.v1 = rotl_a<13>(s.v1); s.v1 ^= s.v0;
+        s.v2 = add_swm(s.v2, s.v3); s.v3 = rotl_a<16>(s.v3); s.v3 ^= s.v2;
+        s.v0 = add_swm(s.v0, s.v3); s.v3 = rotl_a<21>(s.v3); s.v3 ^= s.v0;
+        s.v2 += s.v1; s.v1 = rotl_a<17>(s.v1); s.v1 ^= s.v2;
+    } else if constexpr (V == 9) {
         s.v0 += s.v1; s.v1 = rotl_l<13>(s.v1); s.v1 ^= s.v0; s.v0 = swap32(s.v0);
         s.v2 += s.v3; s.v3 = rotl_l<16>(s.v3); s.v3 ^= s.v2;
         s.v0 += s.v3; s.v3 = rotl_l<21>(s.v3); s.v3 ^= s.v0;
@@ -130,10 +147,10 @@ __device__ __forceinline__ uint64_t lv2(const S& s) { return swap32(s.v2); }
 
 template <int V>
 __device__ __forceinline__ uint64_t fin(S s, uint64_t b) {
-    if constexpr (V == 5) {
-        s.v3 ^= b; round_<5>(s); s.v0 ^= b;
+    if constexpr (V == 5 || V == 10) {
+        s.v3 ^= b; round_<V>(s); s.v0 ^= b;
         s.v2 ^= (0xffull << 32);  // logical v2 ^= 0xff on the stored (swapped) form
-        round_<5>(s); round_<5>(s); round_<5>(s);
+        round_<V>(s); round_<V>(s); round_<V>(s);
         return s.v0 ^ s.v1 ^ lv2(s) ^ s.v3;
     }
     s.v3 ^= b; round_<V>(s); s.v0 ^= b; s.v2 ^= 0xff; round_<V>(s); round_<V>(s); round_<V>(s);
@@ -199,9 +216,9 @@ __global__ __launch_bounds__(BS) void k_hash2(uint64_t n, int k, uint64_t m, uin
     extern __shared__ uint32_t pad[];
     uint64_t j = (uint64_t)blockIdx.x * BS + threadIdx.x;
     if (j >= n) return;
-    constexpr int V = MODE == 3 ? 3 : MODE == 5 ? 5 : MODE == 6 ? 6 : MODE == 7 ? 6 : MODE == 9 ? 9 : 1;
+    constexpr int V = MODE == 3 ? 3 : MODE == 5 ? 5 : MODE == 6 ? 6 : MODE == 7 ? 6 : MODE == 9 ? 9 : MODE == 10 ? 10 : 1;
     S s{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL, 0x7465646279746573ULL};
-    if constexpr (V == 5) s.v2 = swap32(s.v2);  // stored form
+    if constexpr (V == 5 || V == 10) s.v2 = swap32(s.v2);  // stored form
     comp<V>(s, 16); comp<V>(s, j * 0x9E3779B97F4A7C15ULL); comp<V>(s, j);
     uint64_t acc = 0;
     if constexpr (MODE == 2 || MODE == 7) {
@@ -318,7 +335,7 @@ template <int V>
 __global__ void k_hash_check(uint64_t* out) {
     const uint64_t j = threadIdx.x;
     S s{0x736f6d6570736575ULL, 0x646f72616e646f6dULL, 0x6c7967656e657261ULL, 0x7465646279746573ULL};
-    if constexpr (V == 5) s.v2 = swap32(s.v2);
+    if constexpr (V == 5 || V == 10) s.v2 = swap32(s.v2);
     comp<V>(s, 16); comp<V>(s, j * 0x9E3779B97F4A7C15ULL); comp<V>(s, j);
     out[j] = fin<V>(s, 32ull << 56);
 }
@@ -362,6 +379,17 @@ int main(int argc, char** argv) {
         for (int i = 0; i < 64; ++i) bad += h1[i] != h9[i];
         printf("V9 (shift + v_lshl_add_u64 rotates) == V1 hashes: %s\n", bad ? "MISMATCH" : "ok");
     }
+    {
+        uint64_t *c1, *c10;
+        CHECK(hipMalloc(&c1, 64 * 8)); CHECK(hipMalloc(&c10, 64 * 8));
+        hipLaunchKernelGGL(k_hash_check<1>, dim3(1), dim3(64), 0, 0, c1);
+        hipLaunchKernelGGL(k_hash_check<10>, dim3(1), dim3(64), 0, 0, c10);
+        uint64_t h1[64], h10[64];
+        CHECK(hipMemcpy(h1, c1, 512, hipMemcpyDeviceToHost)); CHECK(hipMemcpy(h10, c10, 512, hipMemcpyDeviceToHost));
+        int bad = 0;
+        for (int i = 0; i < 64; ++i) bad += h1[i] != h10[i];
+        printf("V10 (swapped adds as v_mad_u64_u32 + v_add_u32) == V1 hashes: %s\n", bad ? "MISMATCH" : "ok");
+    }
     float t0 = time_ms([&] { hipLaunchKernelGGL(k_hash<0>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
     float t1 = time_ms([&] { hipLaunchKernelGGL(k_hash<1>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
     float t2 = time_ms([&] { hipLaunchKernelGGL(k_hash<2>, dim3(blocks), dim3(256), 0, 0, n, 10, out); }, 5);
@@ -381,6 +409,9 @@ int main(int argc, char** argv) {
         run(k_hash2<9, 256>, 256, 0, "V9 shift+lshl_add rotates + mod, 256 thr");
         run(k_hash2<1, 256>, 256, 0, "V1 + mod, 256 thr (again)");
         run(k_hash2<9, 256>, 256, 0, "V9 shift+lshl_add rotates + mod, 256 thr (again)");
+        run(k_hash2<10, 256>, 256, 0, "V10 mad_u64 swapped adds + mod, 256 thr");
+        run(k_hash2<1, 256>, 256, 0, "V1 + mod, 256 thr (3rd)");
+        run(k_hash2<10, 256>, 256, 0, "V10 mad_u64 swapped adds + mod, 256 thr (again)");
         run(k_hash2<2, 256>, 256, 0, "V1 2-seed interleave + mod, 256 thr");
         run(k_hash2<3, 256>, 256, 0, "V3 addc + mod, 256 thr");
         run(k_hash2<5, 256>, 256, 0, "V5 swap-folded carry adds + mod, 256 thr");
