@@ -119,6 +119,9 @@ def test_hashes_variable_length_unaligned(vbf, ora):
                                       (32, 1, 4_000_003, 4), (24, 1, 777_777, 7), (12, 1, 50_000, 5),
                                       (16, 0, 65536, 32), (100, 1, 1_000_003, 2),
                                       (16, 1, 3_000_000_017, 1), (16, 1, 4294967295, 4),
+                                      # m = 2^32 - 1 (saturated sizing): the SAT kernels' remainders
+                                      (16, 1, 4294967295, 10), (32, 1, 4294967295, 19),
+                                      (24, 1, 4294967295, 9), (8, 1, 4294967295, 4), (16, 0, 4294967295, 10),
                                       # k = 19 (p = 1e-4): two lanes per key for fixed layouts
                                       (16, 1, 3_800_017, 19), (32, 0, 500_009, 19), (24, 1, 2_000_003, 19),
                                       (16, 1, 2_999_999_999, 19),
@@ -296,6 +299,23 @@ def test_saturated_m_config5_shape(vbf, ora):
     np.bitwise_or.at(want, (hs >> np.uint64(5)).astype(np.int64).ravel(),
                      (np.uint32(1) << (hs & np.uint64(31)).astype(np.uint32)).ravel())
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("k", [4, 10, 19, 7])
+def test_saturated_m_variable_length(vbf, ora, k):
+    """m = 2^32 - 1 with runtime-length keys: the SAT kernels (k = 4, 10, 19: end-around-carry
+    remainders, sip13.hpp mod_sat) and a runtime-k class (7) against the oracle's hashes % m."""
+    from velarixdb_amd.keys import pack_offsets
+    from velarixdb_amd.workloads import SEED_CFG3, var_offsets
+    m, n = 4294967295, 60_000
+    off = var_offsets(SEED_CFG3, 7, n)
+    b = pack_offsets(ora.gen_var(SEED_CFG3, 7, off), off)
+    got = gpu_build(vbf, b, m, k, strategy=PARTITIONED)
+    want_idx = np.unique((ora.hashes(b, k) % np.uint64(m)).ravel())
+    nz = np.flatnonzero(got)
+    bits = np.unpackbits(got[nz].view(np.uint8), bitorder="little").reshape(-1, 32)
+    got_idx = np.sort((nz[:, None].astype(np.uint64) * np.uint64(32) + np.arange(32, dtype=np.uint64))[bits.astype(bool)])
+    assert np.array_equal(got_idx, want_idx)
 
 
 def test_edge_cases(vbf, ora):

@@ -188,10 +188,23 @@ __device__ __forceinline__ uint32_t fast_mod31(uint64_t x, uint32_t m, uint64_t 
     return min(r, r - m);
 }
 
-// M31: m <= 2^31 known at launch (a template flag of the calling kernel).
-template <bool M31>
+// x % (2^32 - 1), the reference's saturated size (bf.rs:230-233: every filter of more than 2^32 - 1
+// bits, e.g. config 5): 2^32 = 1 (mod m), so x = hi + lo (mod m).  s = hi + lo < 2^33 - 1, and
+// u = (s mod 2^32) + (s >> 32) <= m, where u == m means 0.  Four full-rate instructions instead of
+// the Barrett step's seven 32x32 products (checked against x % m on the host: edges + 2M random).
+__host__ __device__ __forceinline__ uint32_t mod_sat(uint64_t x) {
+    const uint64_t s = (x & 0xFFFFFFFFull) + (x >> 32);
+    const uint32_t u = (uint32_t)s + (uint32_t)(s >> 32);
+    return u == 0xFFFFFFFFu ? 0u : u;
+}
+
+// M31: m <= 2^31 known at launch (a template flag of the calling kernel); SAT: m == 2^32 - 1.
+template <bool M31, bool SAT = false>
 __device__ __forceinline__ uint32_t mod_m(uint64_t x, uint64_t m, uint64_t mu) {
-    if constexpr (M31)
+    static_assert(!(M31 && SAT), "m = 2^32 - 1 is above 2^31");
+    if constexpr (SAT)
+        return mod_sat(x);
+    else if constexpr (M31)
         return fast_mod31(x, (uint32_t)m, mu);
     else
         return fast_mod(x, m, mu);

@@ -686,7 +686,12 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
             const int fmt = pick_fmt(dk.keys, dk.offsets, dk.stride);
             err = pl.kc <= 12 ? launch_tile_pack_class_a(fmt, dk, pl, ntiles, tiles, pl.ends_t ? endsT : ends, s)
                               : launch_tile_pack_class_b(fmt, dk, pl, ntiles, tiles, pl.ends_t ? endsT : ends, s);
+        } else if (kb.len_prefix && m == 0xFFFFFFFFu &&
+                   (err = launch_tile_pack_sat(pick_fmt(dk.keys, dk.offsets, dk.stride), dk, pl, ntiles, tiles,
+                                               pl.ends_t ? endsT : ends, s)) != hipErrorNotSupported) {
+            // m = 2^32 - 1 (the reference's saturated size): end-around-carry remainders (SAT kernels)
         } else with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
+            err = hipSuccess;
             // m <= 2^31: the one-word remainder (fast_mod31); the runtime-k kernel keeps the general one
             auto pick = [&]<bool S>() {
                 if constexpr (FMT > 0 && S) {  // the 512-thread shape (make_plan: m <= 2^31)

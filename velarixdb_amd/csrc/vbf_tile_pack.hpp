@@ -140,8 +140,9 @@ __host__ __device__ constexpr uint32_t group_words(uint32_t entries) { return (e
 // SB < kSegBits, POS (the multi-SST group pack, vbf_multi_part.hip): segments of 2^SB positions, and
 // every entry's place in the tile image is also written to posv[tile][stash slot][lane] (u16), so
 // the group output pass finds a key's k results without re-reading the image.
+// SAT: m == 2^32 - 1 (the reference's saturated size), remainders by mod_sat (sip13.hpp).
 template <int FMT, bool LP, int K, bool M31, bool C16 = false, int V = 0, int KC = 0, int SB = kSegBits,
-          bool POS = false>
+          bool POS = false, bool SAT = false>
 __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile_pack(DevKeys dk, PartPlan pl,
                                                                                       uint32_t* tiles, uint16_t* ends,
                                                                                       uint16_t* posv) {
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
                 // class kernels: seeds past the runtime k (wave-uniform) leave sentinels
                 if (valid && (SPL == 1 || seed0 + i < (uint32_t)K) && (KC == 0 || (uint32_t)i < pl.k)) {
                     const uint64_t h = FMT > 0 ? seed_hash(q, seed0 + i) : prefix_hash(p, seed0 + i);
-                    idx = mod_m<M31>(h, pl.m, pl.mu);
+                    idx = mod_m<M31, SAT>(h, pl.m, pl.mu);
                     seg_count<C16, SB>(cnt0, idx);
                 }
                 stash[r * KL + i] = idx;
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
             for (uint32_t i = 0; i < pl.k; ++i) {
                 uint32_t idx = kSentinel;
                 if (valid) {
-                    idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
+                    idx = mod_m<M31, SAT>(prefix_hash(p, i), pl.m, pl.mu);
                     seg_count<C16, SB>(cnt0, idx);
                 }
                 stash[ns++] = idx;
@@ -421,6 +422,11 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
 bool group_pack_supported(uint64_t m, uint32_t k, int sb = kByteSegBits);
 PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed, int sb = kByteSegBits);
 uint32_t group_pack_slots(uint32_t k);
+// m == 2^32 - 1 with the length prefix and compiled k (4, 9, 10, 19) on the 1 024-thread shape: the
+// SAT kernels (vbf_partition_sat.hip).  hipErrorNotSupported when none fits (the caller then runs
+// the general m > 2^31 kernel).
+hipError_t launch_tile_pack_sat(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles,
+                                uint16_t* ends, hipStream_t s);
 hipError_t launch_group_pack(const KeyBatch& kb, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                              uint32_t* tiles, uint16_t* endsT, uint16_t* posv, int sb, hipStream_t s);
 
