@@ -500,8 +500,10 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     // needs no run padding and holds 3 072 keys with plain counters, which then skip the packing's
     // VALU (the 512-thread k = 19 K1: 6.18 -> 6.05 ms, matrix3.log; k = 10 even).  Only the
     // 1 024-thread k = 19 shape (two lanes per key: m > 2^31) keeps them, for its 1 536-key tile.
+    // k = 4 above 2 048 segments (m = 2^32 - 1, config 5): 16 KiB of plain counters would cap the
+    // tile at 6 532 keys, packed ones leave room for the 7 168 of seven stash rounds
     pl.c16 = (uint32_t)(!group && (k == 19 || k == 4 || k == 10) &&
-                        (c16env >= 0 ? c16env != 0 : (k == 19 && !pl.k1v)));
+                        (c16env >= 0 ? c16env != 0 : ((k == 19 && !pl.k1v) || (k == 4 && pl.nseg > 2048))));
     if (!fixed && pl.c16) pl.k1v = 0;
     const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : k), fixed, (int)pl.k1v);
     const uint32_t rmax = (uint32_t)(ck || pl.kc ? sh.rounds : rounds_max((int)k));

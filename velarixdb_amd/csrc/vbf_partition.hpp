@@ -44,8 +44,11 @@ __host__ __device__ constexpr int build_spl(int k, bool fixed) { return (k == 19
 __host__ __device__ constexpr int build_kl(int k, bool fixed) {
     return (k + build_spl(k, fixed) - 1) / build_spl(k, fixed);
 }
+// The build's fixed-layout K = 4 kernels stash 7 rounds (28 indices; 56-62 VGPRs, no scratch):
+// 7 168-key tiles where the LDS holds them (m = 2^32 - 1: with packed counters), 17 % fewer
+// k_seg_or runs.  Runtime-length layouts keep 6 (7 spills 12-20 bytes of scratch there).
 __host__ __device__ constexpr int build_rounds_max(int k, bool fixed) {
-    return build_spl(k, fixed) == 1 ? rounds_max(k) : kStash / build_kl(k, fixed);
+    return build_spl(k, fixed) != 1 ? kStash / build_kl(k, fixed) : (k == 4 && fixed) ? 7 : rounds_max(k);
 }
 
 // K1 workgroup shapes (k_tile_pack template parameter V).  V = 0: 1024 threads with the lanes per
