@@ -359,19 +359,21 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
         for (uint32_t t = 0; t < kNsMax; t += 8) {
             if (!FULL && t >= ns) break;
             uint32_t pos[8], val[8];
+            bool live[8];  // FULL: every slot below kNsMax (compile-time per unrolled q) holds an index
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                val[q] = (FULL || t + q < ns) ? stash[t + q] : kSentinel;
-                pos[q] = (FULL || val[q] != kSentinel) ? seg_rank<C16, SB>(cnt0, val[q]) : 0u;
+                val[q] = (t + q < kNsMax && (FULL || t + q < ns)) ? stash[t + q] : kSentinel;
+                live[q] = FULL ? t + q < kNsMax : val[q] != kSentinel;
+                pos[q] = live[q] ? seg_rank<C16, SB>(cnt0, val[q]) : 0u;
             }
             if constexpr (POS) {  // the group pack places every run at its padded place (whole groups)
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
-                    if (FULL || val[q] != kSentinel) pos[q] += gd_get(val[q] >> SB);
+                    if (live[q]) pos[q] += gd_get(val[q] >> SB);
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                if (FULL || val[q] != kSentinel) {
+                if (live[q]) {
                     const uint32_t gb = __umul24(pos[q] >> 3, 4u * kGroupWords) + img0, e7 = pos[q] & 7;
                     *reinterpret_cast<lds_u16*>(static_cast<uintptr_t>(gb + 2 * e7)) = (uint16_t)val[q];
                     (void)__hip_atomic_fetch_or(reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(gb + 16)),
@@ -384,10 +386,9 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
                 uint32_t* pv = reinterpret_cast<uint32_t*>(posv);
 #pragma unroll
                 for (int q = 0; q < 8; q += 2)
-                    if (FULL || val[q] != kSentinel || val[q + 1] != kSentinel)
+                    if (live[q] || live[q + 1])
                         pv[((uint64_t)tile * ((kNsMax + 1) / 2) + (t + q) / 2) * BS + tid] =
-                            ((FULL || val[q] != kSentinel) ? pos[q] : 0u) |
-                            (((FULL || val[q + 1] != kSentinel) ? pos[q + 1] : 0u) << 16);
+                            (live[q] ? pos[q] : 0u) | ((live[q + 1] ? pos[q + 1] : 0u) << 16);
             }
         }
     };
