@@ -346,60 +346,37 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     // rank + place, 8 returning LDS atomics in flight before their results are used
     // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
     constexpr uint32_t kNsMax = KK > 0 ? (uint32_t)(RMK * KL) : (uint32_t)kStash;
-    // LDS byte address of the image: a group is 20 bytes, so an entry's u16 sits at byte
-    // 20 * (pos >> 3) + 2 * (pos & 7) and its group's nibble word at 20 * (pos >> 3) + 16
-    // (24-bit multiplies: pos < 2^16)
-    const uint32_t img0 = (pl.cnt_words + 16 + kLenBuckets + pl.gd_words) * 4;  // == smem (LDS starts at cnt)
-    typedef __attribute__((address_space(3))) uint16_t lds_u16;
-    // FULL (wave-uniform, speed only): every stash slot of the tile holds an index (a whole tile
-    // of a compiled-k kernel with one lane per key) -- no sentinel tests, no divergent branches
-    auto place_all = [&](auto fullc) {
-        constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-        for (uint32_t t = 0; t < kNsMax; t += 8) {
-            if (!FULL && t >= ns) break;
-            uint32_t pos[8], val[8];
-            bool live[8];  // FULL: every slot below kNsMax (compile-time per unrolled q) holds an index
+    for (uint32_t t = 0; t < kNsMax; t += 8) {
+        if (t >= ns) break;
+        uint32_t pos[8], val[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                val[q] = (t + q < kNsMax && (FULL || t + q < ns)) ? stash[t + q] : kSentinel;
-                live[q] = FULL ? t + q < kNsMax : val[q] != kSentinel;
-                pos[q] = live[q] ? seg_rank<C16, SB>(cnt0, val[q]) : 0u;
-            }
-            if constexpr (POS) {  // the group pack places every run at its padded place (whole groups)
+        for (int q = 0; q < 8; ++q) {
+            val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
+            pos[q] = val[q] != kSentinel ? seg_rank<C16, SB>(cnt0, val[q]) : 0u;
+        }
+        if constexpr (POS) {  // the group pack places every run at its padded place (whole groups)
 #pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (live[q]) pos[q] += gd_get(val[q] >> SB);
-            }
+            for (int q = 0; q < 8; ++q)
+                if (val[q] != kSentinel) pos[q] += gd_get(val[q] >> SB);
+        }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                if (live[q]) {
-                    const uint32_t gb = __umul24(pos[q] >> 3, 4u * kGroupWords) + img0, e7 = pos[q] & 7;
-                    *reinterpret_cast<lds_u16*>(static_cast<uintptr_t>(gb + 2 * e7)) = (uint16_t)val[q];
-                    (void)__hip_atomic_fetch_or(reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(gb + 16)),
-                                                ((val[q] >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4),
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-            }
-            if constexpr (POS) {  // coalesced: for a pair of stash slots the lanes write consecutive u32
-                static_assert(KK > 0, "the group pack runs compiled k");
-                uint32_t* pv = reinterpret_cast<uint32_t*>(posv);
-#pragma unroll
-                for (int q = 0; q < 8; q += 2)
-                    if (live[q] || live[q + 1])
-                        pv[((uint64_t)tile * ((kNsMax + 1) / 2) + (t + q) / 2) * BS + tid] =
-                            (live[q] ? pos[q] : 0u) | ((live[q + 1] ? pos[q + 1] : 0u) << 16);
+        for (int q = 0; q < 8; ++q) {
+            if (val[q] != kSentinel) {
+                const uint32_t g = (pos[q] >> 3) * kGroupWords, e7 = pos[q] & 7;
+                lo[g * 2 + e7] = (uint16_t)val[q];
+                atomicOr(&smem[g + 4], ((val[q] >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4));
             }
         }
-    };
-    constexpr bool kCanFull = KK > 0 && KC == 0 && SPL == 1 && RMK * KL == (int)kNsMax;
-    if constexpr (kCanFull) {
-        if (nk == (uint32_t)RMK * kKeysPerRound && pl.R == (uint32_t)RMK)
-            place_all(std::true_type{});
-        else
-            place_all(std::false_type{});
-    } else {
-        place_all(std::false_type{});
+        if constexpr (POS) {  // coalesced: for a pair of stash slots the lanes write consecutive u32
+            static_assert(KK > 0, "the group pack runs compiled k");
+            uint32_t* pv = reinterpret_cast<uint32_t*>(posv);
+#pragma unroll
+            for (int q = 0; q < 8; q += 2)
+                if (val[q] != kSentinel || val[q + 1] != kSentinel)
+                    pv[((uint64_t)tile * ((kNsMax + 1) / 2) + (t + q) / 2) * BS + tid] =
+                        (val[q] != kSentinel ? pos[q] : 0u) | ((val[q + 1] != kSentinel ? pos[q + 1] : 0u) << 16);
+        }
     }
     __syncthreads();
     // cnt[s] = start(s) + count(s) = the end of segment s's run.  The last group's low halves past
