@@ -39,6 +39,8 @@ for s in $STEPS; do
     abprev19) run ab_prev19 600 env AB_LIB=velarixdb_amd/libvbf_prev.so tools/ab_lib.sh 3 --bits-per-key 19 ;;
     abprev3) run ab_prev3 600 env AB_LIB=velarixdb_amd/libvbf_prev.so tools/ab_lib.sh 2 --config 3 --steps 5 --warmup 1 ;;
     abprev5) for i in 1 2; do for lib in "" velarixdb_amd/libvbf_prev.so; do run bench_cfg5_prev$i${lib:+_prev} 600 env VBF_LIB=$lib python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline; grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_cfg5_prev$i${lib:+_prev}.log"; done; done ;;
+    probe5) run bench_cfg5_probe 600 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    probemultitests) run pytest_probe_multi 900 python -u -m pytest tests/test_gpu_probe.py tests/test_gpu_multi.py tests/test_gpu_parity.py tests/test_gpu_scale.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     paritytest) run pytest_parity 900 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     absat5) for v in 0 1 0 1; do run bench_cfg5_sat$v 600 env VBF_SAT=$v python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline; grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_cfg5_sat$v.log"; done ;;
     prof5) (cd /tmp && run prof5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5" -o run -- python3 "$ROOT/bench.py" --config 5 --steps 3 --warmup 1 --no-cpu-baseline) || exit $? ;;

@@ -22,14 +22,18 @@ static_assert(kSegBits == 20, "probe entries hold a 12-bit key id above the 20-b
 
 // SB: segment = 2^SB filter positions (bits of one filter: 20; bytes of an interleaved group of
 // filters, vbf_multi_part.hip: 17).  An entry is (tile-local key id << SB) | offset in segment.
-template <int FMT, bool LP, int K, bool M31, int SB>
+// SAT: m == 2^32 - 1, remainders by mod_sat (sip13.hpp).
+// Per segment one LDS word holds the run's count (-> start -> end) in its low half and its padded
+// start in the high half: both stay below 2^16 (C + 7 * nseg <= cap <= 65535, probe_partition_
+// supported), so one scan of the words scans both and no half carries into the other -- half the
+// counters' LDS of two u32 arrays, which at m = 2^32 - 1 (4 096 segments) buys 33 % larger tiles.
+template <int FMT, bool LP, int K, bool M31, int SB, bool SAT = false>
 __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan pl, uint32_t* tiles, uint16_t* ends) {
     constexpr uint32_t kOff = (1u << SB) - 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     uint32_t* ent = smem;               // C entries
-    uint32_t* cnt = ent + pl.C;         // nseg_pad: counts -> starts -> ends
-    uint32_t* pst = cnt + pl.nseg_pad;  // nseg_pad: padded starts
-    uint32_t* wsum = pst + pl.nseg_pad; // 16
+    uint32_t* cnt = ent + pl.C;         // nseg_pad: count | padded count << 16 -> starts -> end | padded start
+    uint32_t* wsum = cnt + pl.nseg_pad; // 16
     const uint32_t tid = threadIdx.x;
     for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
     __syncthreads();
@@ -52,7 +56,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
             for (int i = 0; i < K; ++i) {
                 uint32_t idx = kSentinel;
                 if (valid) {
-                    idx = mod_m<M31>(FMT > 0 ? seed_hash(q, i) : prefix_hash(p, i), pl.m, pl.mu);
+                    idx = mod_m<M31, SAT>(FMT > 0 ? seed_hash(q, i) : prefix_hash(p, i), pl.m, pl.mu);
                     atomicAdd(&cnt[idx >> SB], 1u);
                 }
                 stash[r * K + i] = idx;
@@ -80,11 +84,9 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
         }
     }
     __syncthreads();
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) pst[s] = (cnt[s] + 7) & ~7u;
+    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] |= ((cnt[s] + 7) & ~7u) << 16;
     __syncthreads();
     block_exclusive_scan(cnt, pl.nseg, wsum);
-    __syncthreads();
-    block_exclusive_scan(pst, pl.nseg, wsum);
     __syncthreads();
     const uint32_t per = K > 0 ? (uint32_t)K : pl.k;
     // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
@@ -96,7 +98,7 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> SB], 1u) : 0u;
+            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> SB], 1u) & 0xFFFFu : 0u;
         }
 #pragma unroll
         for (int q = 0; q < 8; ++q)
@@ -111,8 +113,8 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
     uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.cap;
     uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nseg;
     for (uint32_t s = grp; s < pl.nseg; s += kPBlock / 8) {
-        const uint32_t st = s ? cnt[s - 1] : 0, en = cnt[s], c = en - st, pc = (c + 7) & ~7u;
-        const uint32_t d = pst[s];
+        const uint32_t st = s ? cnt[s - 1] & 0xFFFFu : 0, en = cnt[s] & 0xFFFFu, c = en - st, pc = (c + 7) & ~7u;
+        const uint32_t d = cnt[s] >> 16;
         for (uint32_t x = q; x < pc; x += 8) out[d + x] = ent[std::min(st + x, en - 1)];
         if (q == 0) eo[s] = (uint16_t)(d + pc);
     }
@@ -579,13 +581,13 @@ ProbePlan make_probe_plan(uint32_t m, uint32_t k, int sb) {
     pl.nseg = (uint32_t)(((uint64_t)m + (1u << sb) - 1) >> sb);
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
     const uint32_t rmax = (uint32_t)rounds_max((int)k);
-    const int64_t avail = (int64_t)(kLdsPerCu / 2) - 64 - 8 * (int64_t)pl.nseg_pad;
+    const int64_t avail = (int64_t)(kLdsPerCu / 2) - 64 - 4 * (int64_t)pl.nseg_pad;
     const int64_t kt = std::min<int64_t>(std::min<int64_t>((int64_t)rmax * kPBlock, avail / 4 / k), 4096);
     pl.KT = (uint32_t)std::max<int64_t>(kt, 1);
     pl.R = (pl.KT + kPBlock - 1) / kPBlock;
     pl.C = pl.KT * k;
     pl.cap = (pl.C + 7 * pl.nseg + 31) & ~31u;  // multiple of 32: k_probe_out reads result dwords
-    pl.lds1 = (pl.C + 2 * pl.nseg_pad + 16) * 4;
+    pl.lds1 = (pl.C + pl.nseg_pad + 16) * 4;
     return pl;
 }
 
@@ -625,6 +627,11 @@ hipError_t launch_probe_pack_fmt(const DevKeys& dk, const ProbePlan& pl, uint32_
                        : k_probe_pack<FMT, LP, 0, false, SB>;
     };
     auto fn = pl.m <= (1ull << 31) ? pick.template operator()<true>() : pick.template operator()<false>();
+    if constexpr (LP && SB == kSegBits) {  // m = 2^32 - 1 (the reference's saturated size): SAT kernels
+        if (pl.m == 0xFFFFFFFFull && (k == 4 || k == 10 || k == 19))
+            fn = k == 4 ? k_probe_pack<FMT, LP, 4, false, SB, true>
+               : k == 10 ? k_probe_pack<FMT, LP, 10, false, SB, true> : k_probe_pack<FMT, LP, 19, false, SB, true>;
+    }
     hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)pl.lds1);
     if (err == hipSuccess) hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
