@@ -123,9 +123,9 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32
 
 # rocprofv3 names of the build's kernels, and the summary of the same command, per (key bytes, k)
 ROCPROF = {
-    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true, false, 1, 0, 20, false>",
+    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true, false, 1, 0, 20, false, false>",
                 "seg_or": "k_seg_or<6, 1024, 5, 8>"}, "profiles/r04/bench_default_kernel_stats.csv"),
-    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true, false, 1, 0, 20, false>",
+    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true, false, 1, 0, 20, false, false>",
                 "seg_or": "k_seg_or<6, 1024, 4, 8>"}, "profiles/r04/bench_k19_kernel_stats.csv"),
 }
 
@@ -158,8 +158,8 @@ def pmc_traffic(name, kernel=None):
             with open(path) as f:
                 d = json.load(f)
             per_kernel = None
-            # round 4 added defaulted template arguments (KC, SB, POS) to k_tile_pack's name
-            norm = lambda x: x.replace(", 0, 20, false>", ">")
+            # round 4 added defaulted template arguments (KC, SB, POS, SAT) to k_tile_pack's name
+            norm = lambda x: x.replace(", 0, 20, false, false>", ">").replace(", 0, 20, false>", ">")
             for kname, kv in d.get("kernels", {}).items():
                 if kernel and norm(kernel) in norm(kname):
                     per_kernel = kv["read_bytes"] + kv["write_bytes"]

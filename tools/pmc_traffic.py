@@ -30,7 +30,8 @@ def main(fetch_csv, write_csv, out):
     for name in sorted(set(fetch) | set(write)):
         if not any(b in name for b in BUILD_KERNELS):
             continue
-        if ", 20, true>" in name or ", 17, true>" in name:  # the probes' position-table pack (round 4)
+        # the probes' position-table pack (round 4; POS, then SAT in the name)
+        if any(t in name for t in (", 20, true>", ", 17, true>", ", 20, true, false>", ", 17, true, false>")):
             continue
         rd = fetch.get(name, 0.0) * 1024 * 2
         wr = write.get(name, 0.0) * 1024
