@@ -34,6 +34,7 @@ for s in $STEPS; do
     benchstagger14) run bench_stagger14 300 env VBF_STAGGER=14 python bench.py --no-cpu-baseline ;;
     ablate) run ablate 300 python tools/ablate.py ;;
     ubhash) run ubench_hash 300 ./tools/ubench hash ;;
+    overlap) run overlap 300 ./tools/overlap ;;
     pmcicache) (cd /tmp && run pmcicache 600 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcicache" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;
     abprev2) run ab_prev2 600 env AB_LIB=velarixdb_amd/libvbf_prev.so tools/ab_lib.sh 3 ;;
     abprev19) run ab_prev19 600 env AB_LIB=velarixdb_amd/libvbf_prev.so tools/ab_lib.sh 3 --bits-per-key 19 ;;
