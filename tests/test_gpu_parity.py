@@ -122,6 +122,7 @@ def test_hashes_variable_length_unaligned(vbf, ora):
                                       # m = 2^32 - 1 (saturated sizing): the SAT kernels' remainders
                                       (16, 1, 4294967295, 10), (32, 1, 4294967295, 19),
                                       (24, 1, 4294967295, 9), (8, 1, 4294967295, 4), (16, 0, 4294967295, 10),
+                                      (16, 1, 4294967295, 14), (32, 1, 4294967295, 7), (16, 1, 4294967295, 29),
                                       # k = 19 (p = 1e-4): two lanes per key for fixed layouts
                                       (16, 1, 3_800_017, 19), (32, 0, 500_009, 19), (24, 1, 2_000_003, 19),
                                       (16, 1, 2_999_999_999, 19),

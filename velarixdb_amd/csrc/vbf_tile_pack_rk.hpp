@@ -3,6 +3,8 @@
 // (vbf_partition_rk_a.hip: classes 5, 8, 12; vbf_partition_rk_b.hip: 16, 21, 24, 32), which the build
 // compiles in parallel with the rest of the library.
 #pragma once
+#include <stdlib.h>
+
 #include "vbf_tile_pack.hpp"
 
 namespace vbf {
@@ -20,13 +22,21 @@ hipError_t launch_tile_pack_class_a(int fmt, const DevKeys& dk, const PartPlan& 
 hipError_t launch_tile_pack_class_b(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                                     uint32_t* tiles, uint16_t* ends, hipStream_t s);
 
+// VBF_SAT=0 (A/B, speed only): Barrett remainders at m = 2^32 - 1 as well (vbf_partition_sat.hip)
+inline bool sat_enabled() {
+    static const int on = [] { const char* e = getenv("VBF_SAT"); return e ? atoi(e) : 1; }();
+    return on != 0;
+}
+
 // One class kernel: the segment counters sit at LDS address 0 (no static LDS may precede them),
 // the dynamic LDS request is the plan's.
 template <int FMT, int KC>
 hipError_t launch_one_class(const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles, uint16_t* ends,
                             hipStream_t s) {
-    auto fn = pl.m <= (1ull << 31) ? k_tile_pack<FMT, true, 0, true, false, 1, KC>
-                                   : k_tile_pack<FMT, true, 0, false, false, 1, KC>;
+    // m = 2^32 - 1 (the reference's saturated size): the end-around-carry remainder (SAT)
+    auto fn = pl.m <= (1ull << 31)        ? k_tile_pack<FMT, true, 0, true, false, 1, KC>
+              : pl.m == 0xFFFFFFFFull && sat_enabled() ? k_tile_pack<FMT, true, 0, false, false, 1, KC, kSegBits, false, true>
+                                                  : k_tile_pack<FMT, true, 0, false, false, 1, KC>;
     hipFuncAttributes fa{};
     hipError_t err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
     if (err == hipSuccess && fa.sharedSizeBytes != 0) err = hipErrorInvalidKernelFile;
