@@ -32,8 +32,11 @@ __global__ void k_gen(uint32_t* bnd, uint32_t ntiles, uint32_t nseg, uint32_t me
     atomicMax(used, e);
 }
 
-// GE entries per group, GB bytes per group
-template <int GE, int GB>
+// GE entries per group, GB bytes per group; LOC (g20 only): each run's lane writes its groups'
+// (run, group index) into a per-wave LDS slot table and the group lanes read their slot -- one LDS
+// write per group and one read instead of the 6-step binary search over the prefix (ds_bpermute)
+// plus two shuffles
+template <int GE, int GB, bool LOC = false>
 __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles,
                                                uint32_t nseg, uint32_t tile_bytes, uint32_t* out) {
     extern __shared__ uint32_t lds[];
@@ -56,16 +59,30 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
             if (lane >= (uint32_t)o) incl += y;
         }
         const uint32_t excl = incl - ch, total = (uint32_t)__shfl((int)incl, 63);
+        uint32_t* slot = lds + 32768 + wave * 512;
+        if constexpr (LOC) {
+            for (uint32_t x = 0; x < ch && excl + x < 512; ++x) slot[excl + x] = lane | ((st / 8 + x) << 6);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         for (uint32_t c = lane; c < total; c += 64) {
-            uint32_t r = 0;
+            uint32_t r = 0, gi;
+            if (LOC && c < 512) {
+                const uint32_t e = slot[c];
+                r = e & 63u;
+                gi = e >> 6;
+            } else {
 #pragma unroll
-            for (int sft = 32; sft; sft >>= 1)
-                if ((uint32_t)__shfl((int)excl, (int)r + sft) <= c) r += sft;
-            const uint32_t rv = (uint32_t)__shfl((int)v, (int)r), rex = (uint32_t)__shfl((int)excl, (int)r);
+                for (int sft = 32; sft; sft >>= 1)
+                    if ((uint32_t)__shfl((int)excl, (int)r + sft) <= c) r += sft;
+                const uint32_t rv = (uint32_t)__shfl((int)v, (int)r), rex = (uint32_t)__shfl((int)excl, (int)r);
+                gi = (rv & 0xFFFFu) / (GE ? GE : 8) + (c - rex);
+            }
             const uint8_t* tile = img + (uint64_t)min(t0 + r, ntiles - 1) * tile_bytes;
-            const uint32_t gi = (rv & 0xFFFFu) / (GE ? GE : 8) + (c - rex);
             uint4 l;
             if (GB == 0) {  // raw: aligned 16-byte chunks of the run's byte range (GE = 8, 20-byte groups)
+                const uint32_t rv = (uint32_t)__shfl((int)v, (int)r), rex = (uint32_t)__shfl((int)excl, (int)r);
                 l = *reinterpret_cast<const uint4*>(tile + ((rv & 0xFFFFu) / 8 * 20 / 16 + (c - rex)) * 16);
                 acc ^= l.x ^ l.y ^ l.z ^ l.w;
             } else if (GB == 16) {
@@ -84,19 +101,20 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
     if (threadIdx.x == 0 && lds[0] == 0x12345678u) out[0] = acc;
 }
 
-template <int GE, int GB>
+template <int GE, int GB, bool LOC = false>
 static float run(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles, uint32_t nseg, uint32_t tile_bytes,
                  uint32_t* out) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    const uint32_t lds = 128 * 1024;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_read<GE, GB>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
-    hipLaunchKernelGGL((k_read<GE, GB>), dim3(nseg), dim3(1024), lds, 0, img, bnd, ntiles, nseg, tile_bytes, out);
+    const uint32_t lds = 128 * 1024 + 16 * 512 * 4;  // bitmap + per-wave slot tables (LOC)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_read<GE, GB, LOC>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL((k_read<GE, GB, LOC>), dim3(nseg), dim3(1024), lds, 0, img, bnd, ntiles, nseg, tile_bytes, out);
     (void)hipEventRecord(e0);
     for (int r = 0; r < 5; ++r)
-        hipLaunchKernelGGL((k_read<GE, GB>), dim3(nseg), dim3(1024), lds, 0, img, bnd, ntiles, nseg, tile_bytes, out);
+        hipLaunchKernelGGL((k_read<GE, GB, LOC>), dim3(nseg), dim3(1024), lds, 0, img, bnd, ntiles, nseg, tile_bytes,
+                           out);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms = 0;
@@ -108,7 +126,7 @@ int main() {
     struct Cfg { const char* name; uint32_t ntiles, nseg, mean; };
     // k = 10: 100M keys / 3072 per tile, m = 1e9; k = 19: 100M / 1536, m = 1.9e9; and 19 with a
     // 3072-key tile (one k_tile_pack workgroup per CU)
-    const Cfg cfgs[] = {{"k10", 32553, 954, 32}, {"k19", 65105, 1812, 16}, {"k19x2", 32553, 1812, 32}};
+    const Cfg cfgs[] = {{"k10", 32553, 954, 32}, {"k19", 65105, 1812, 16}, {"cfg5", 69755, 4096, 7}};
     for (const Cfg& c : cfgs) {
         uint32_t *bnd, *used, *out;
         const uint64_t nb = (uint64_t)c.ntiles * c.nseg;
@@ -117,7 +135,7 @@ int main() {
         hipLaunchKernelGGL(k_gen, dim3((c.ntiles + 255) / 256), dim3(256), 0, 0, bnd, c.ntiles, c.nseg, c.mean, used);
         uint32_t cap = 0;
         (void)hipMemcpy(&cap, used, 4, hipMemcpyDeviceToHost);
-        for (int fmt = 0; fmt < 3; ++fmt) {
+        for (int fmt : {0, 3}) {
             const uint32_t tile_bytes = fmt != 1 ? ((cap + 7) / 8 * 20 + 16 + 15) & ~15u : ((cap + 5) / 6 * 16 + 16);
             const uint64_t bytes = (uint64_t)c.ntiles * tile_bytes + 4096;
             uint8_t* img;
@@ -126,9 +144,11 @@ int main() {
             for (int rep = 0; rep < 2; ++rep) {
                 const float ms = fmt == 0   ? run<8, 20>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
                                  : fmt == 1 ? run<6, 16>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
+                                 : fmt == 3 ? run<8, 20, true>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
                                             : run<8, 0>(img, bnd, c.ntiles, c.nseg, tile_bytes, out);
                 printf("%-6s %s %.3f ms  (%.1f G runs/s, %u B per tile, %.2f GB image)\n", c.name,
-                       fmt == 0 ? "g20" : fmt == 1 ? "g16" : "raw20", ms, (double)nb / (ms * 1e-3) / 1e9, tile_bytes,
+                       fmt == 0 ? "g20" : fmt == 1 ? "g16" : fmt == 3 ? "g20loc" : "raw20", ms,
+                       (double)nb / (ms * 1e-3) / 1e9, tile_bytes,
                        (double)c.ntiles * tile_bytes / 1e9);
             }
             (void)hipFree(img);
