@@ -599,13 +599,29 @@ def bench_cfg5(ctx, args):
     torch.cuda.synchronize()
     fp = ctx.sum_over_ranks(int(cnt.item()))
     value = N * args.steps / wall
+    # as config 2: algorithmic bytes (key bytes + this rank's share of the filter write) over the
+    # dominant kernel's mean launch; the build runs in chunks, so per launch = the chunk's keys
+    ph = phase_report(phases, args.steps)
+    bpk = L + m / (8.0 * N)
+    dom = max(ph, key=lambda q: ph[q]["ms_per_launch"] * ph[q]["launches"]) if ph else None
+    roofline = None
+    if dom:
+        per_step = max(1.0, ph[dom]["launches"] / args.steps)
+        achieved = n / per_step * bpk / (ph[dom]["ms_per_launch"] / 1e3) / 1e9
+        traffic, traffic_build, traffic_src = (pmc_traffic("traffic_config5.json", "k_tile_pack<32, true, 4, false")
+                                               if N == 1_000_000_000 and ctx.world == 1 and args.strategy != 1
+                                               else (None, None, None))
+        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_per_chunk": traffic_build,
+                    "traffic_source": traffic_src, "kernel": dom, "kernel_ms": ph[dom]["ms_per_launch"],
+                    "launches_per_step": per_step, "algorithmic_bytes_per_key": bpk, "phases": ph}
     return {
         "metric": "Bloom build keys/s (1B-key single filter across GPUs)", "value": value,
         "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "u64", "data": "synthetic", "key_gib_per_s": value * L / 2**30,
         "config": {"workload": "config5: %d x 32B keys, 15 bits/key -> m=%d (u32-saturated), k=%d; OR all-reduce over %d ranks" % (N, m, k, ctx.world)},
-        "build_kernel_ms": float(np.mean(kms)), "probe_sweep_keys_per_s": N / sweep,
+        "build_kernel_ms": float(np.mean(kms)), "roofline": roofline, "probe_sweep_keys_per_s": N / sweep,
         "negatives": {"n": nn * ctx.world, "false_positives": fp, "fpr": fp / (nn * ctx.world)},
     }
 

@@ -79,6 +79,8 @@ for s in $STEPS; do
     ubench) run ubench 300 ./tools/ubench ;;
     rdflat) run rdflat 300 ./tools/rdflat ;;
     pmcrdflat) (cd /tmp && run pmc_rdflat 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_rdflat" -o run -- "$ROOT/tools/rdflat") || exit $? ;;
+    pmc2_5) (cd /tmp && run pmc2_5 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc2_5" -o run -- python3 "$ROOT/bench.py" --config 5 --steps 1 --warmup 1 --no-cpu-baseline --neg-keys 1000000) || exit $? ;;
+    pmc3_5) (cd /tmp && run pmc3_5 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc3_5" -o run -- python3 "$ROOT/bench.py" --config 5 --steps 1 --warmup 1 --no-cpu-baseline --neg-keys 1000000) || exit $? ;;
     pmc2_3) (cd /tmp && run pmc2_3 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc2_3" -o run -- python3 "$ROOT/bench.py" --config 3 --steps 2 --warmup 1 --no-cpu-baseline --neg-keys 1000000) || exit $? ;;
     pmc3_3) (cd /tmp && run pmc3_3 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc3_3" -o run -- python3 "$ROOT/bench.py" --config 3 --steps 2 --warmup 1 --no-cpu-baseline --neg-keys 1000000) || exit $? ;;
     pmcsq3) (cd /tmp && run pmcsq3 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcsq3" -o run -- python3 "$ROOT/bench.py" --config 3 --steps 2 --warmup 1 --no-cpu-baseline --neg-keys 1000000) || exit $? ;;
