@@ -505,6 +505,12 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     pl.c16 = (uint32_t)(!group && (k == 19 || k == 4 || k == 10) &&
                         (c16env >= 0 ? c16env != 0 : ((k == 19 && !pl.k1v) || (k == 4 && pl.nseg > 2048))));
     if (!fixed && pl.c16) pl.k1v = 0;
+    // VBF_K1_4=1 (A/B, speed only): k = 4 at m = 2^32 - 1 with a fixed layout and packed counters on
+    // the 512-thread shape -- only the SAT kernels have it (vbf_partition_sat.hip), so VBF_SAT must
+    // be on as well
+    static const int k14env = [] { const char* e = getenv("VBF_K1_4"); return e ? atoi(e) : 0; }();
+    static const int satenv = [] { const char* e = getenv("VBF_SAT"); return e ? atoi(e) : 1; }();
+    if (k14env == 1 && satenv != 0 && k == 4 && fixed && lp && m == 0xFFFFFFFFu && !group && pl.c16) pl.k1v = 1;
     const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : k), fixed, (int)pl.k1v);
     const uint32_t rmax = (uint32_t)(ck || pl.kc ? sh.rounds : rounds_max((int)k));
     const uint32_t kpr = (uint32_t)sh.bs / (uint32_t)(ck ? sh.spl : 1);  // keys per round

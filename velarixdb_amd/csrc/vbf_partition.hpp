@@ -63,7 +63,8 @@ struct K1Shape {
     int bs, spl, kl, rounds;
 };
 __host__ __device__ constexpr K1Shape k1_shape(int k, bool fixed, int v) {
-    if (v == 1) return K1Shape{512, 1, k, kStashWide / k < 6 ? kStashWide / k : 6};
+    // k = 4 on this shape (m = 2^32 - 1, VBF_K1_4): fourteen rounds, a 7 168-key tile
+    if (v == 1) return K1Shape{512, 1, k, k == 4 ? 14 : kStashWide / k < 6 ? kStashWide / k : 6};
     return K1Shape{kPBlock, build_spl(k, fixed), build_kl(k, fixed), build_rounds_max(k, fixed)};
 }
 

@@ -16,6 +16,10 @@ template <int FMT, int K, bool C16>
 static hipError_t launch_sat(const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles,
                              uint16_t* ends, hipStream_t s) {
     auto fn = k_tile_pack<FMT, true, K, false, C16, 0, 0, kSegBits, false, true>;
+    if constexpr (K == 4 && FMT > 0 && C16) {  // VBF_K1_4: the 512-thread shape (make_plan)
+        if (pl.k1v) fn = k_tile_pack<FMT, true, 4, false, true, 1, 0, kSegBits, false, true>;
+    }
+    if (pl.k1v && !(K == 4 && FMT > 0 && C16)) return hipErrorNotSupported;
     // the segment counters sit at LDS address 0: no static LDS may precede them
     hipFuncAttributes fa{};
     hipError_t err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
@@ -24,7 +28,8 @@ static hipError_t launch_sat(const DevKeys& dk, const PartPlan& pl, uint32_t nti
         err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)pl.lds1);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends, (uint16_t*)nullptr);
+    hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles, ends,
+                       (uint16_t*)nullptr);
     return hipGetLastError();
 }
 
@@ -48,7 +53,7 @@ hipError_t launch_tile_pack_sat(int fmt, const DevKeys& dk, const PartPlan& pl, 
                                 uint16_t* ends, hipStream_t s) {
     // VBF_SAT=0 (A/B, speed only): the general m > 2^31 kernels with the Barrett remainder
     static const int on = [] { const char* e = getenv("VBF_SAT"); return e ? atoi(e) : 1; }();
-    if (!on || pl.m != 0xFFFFFFFFull || pl.k1v || pl.kc) return hipErrorNotSupported;
+    if (!on || pl.m != 0xFFFFFFFFull || (pl.k1v && pl.k != 4) || pl.kc) return hipErrorNotSupported;
     switch (fmt) {
         case 16: return launch_sat_fmt<16>(dk, pl, ntiles, tiles, ends, s);
         case 32: return launch_sat_fmt<32>(dk, pl, ntiles, tiles, ends, s);
