@@ -107,20 +107,25 @@ __device__ __forceinline__ void block_exclusive_scan(uint32_t* v, uint32_t n, ui
 }
 
 // The same over u16 counts packed two per word (count of s = half s & 1 of v[s >> 1]), in place;
-// n <= 4 * kPBlock, every start must fit 16 bits (the caller's CP <= 65535).
-template <bool EVEN = false>
+// PER counts (PER / 2 words) per thread: n <= PER * blockDim.x (the 512-thread K1 shape with 4 096
+// segments takes PER = 8), every start must fit 16 bits (the caller's CP <= 65535).
+template <bool EVEN = false, int PER = 4>
 __device__ __forceinline__ void block_exclusive_scan16(uint32_t* v, uint32_t n, uint32_t* wsum) {
+    static_assert(PER % 2 == 0, "whole words per thread");
+    constexpr int PW = PER / 2;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t loc[4];
+    const uint32_t nw = (n + 1) / 2;
+    uint32_t loc[PER];
     uint32_t sum = 0;
-    const uint32_t w0 = tid * 2 < (n + 1) / 2 ? v[tid * 2] : 0u;
-    const uint32_t w1 = tid * 2 + 1 < (n + 1) / 2 ? v[tid * 2 + 1] : 0u;
-    const uint32_t raw[4] = {w0 & 0xFFFFu, w0 >> 16, w1 & 0xFFFFu, w1 >> 16};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t c = tid * 4 + q < n ? raw[q] : 0u;
-        loc[q] = EVEN ? (c + 1) & ~1u : c;
-        sum += loc[q];
+    for (int w = 0; w < PW; ++w) {
+        const uint32_t x = tid * PW + w < nw ? v[tid * PW + w] : 0u;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t c = tid * PER + 2 * w + h < n ? (x >> (16 * h)) & 0xFFFFu : 0u;
+            loc[2 * w + h] = EVEN ? (c + 1) & ~1u : c;
+            sum += loc[2 * w + h];
+        }
     }
     uint32_t incl = sum;
 #pragma unroll
@@ -134,9 +139,13 @@ __device__ __forceinline__ void block_exclusive_scan16(uint32_t* v, uint32_t n, 
 #pragma unroll
     for (int o = 8; o; o >>= 1) before += __shfl_xor(before, o);
     before = (uint32_t)__shfl((int)before, 0);
-    const uint32_t r0 = before + incl - sum, r1 = r0 + loc[0], r2 = r1 + loc[1], r3 = r2 + loc[2];
-    if (tid * 2 < (n + 1) / 2) v[tid * 2] = r0 | (r1 << 16);
-    if (tid * 2 + 1 < (n + 1) / 2) v[tid * 2 + 1] = r2 | (r3 << 16);
+    uint32_t run = before + incl - sum;
+#pragma unroll
+    for (int w = 0; w < PW; ++w) {
+        const uint32_t r0 = run, r1 = r0 + loc[2 * w];
+        run = r1 + loc[2 * w + 1];
+        if (tid * PW + w < nw) v[tid * PW + w] = r0 | (r1 << 16);
+    }
 }
 
 // Compute units of the current device, cached per device: the segment kernels run one workgroup

@@ -320,7 +320,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
         __syncthreads();
         block_exclusive_scan<false, SPER>(cnt, pl.nseg, wsum);
         __syncthreads();
-        block_exclusive_scan16(gd, pl.nseg, wsum);
+        block_exclusive_scan16<false, SPER>(gd, pl.nseg, wsum);
         __syncthreads();
         for (uint32_t w = tid; w < (pl.nseg + 1) / 2; w += BS) {
             const uint32_t s0 = 2 * w, s1 = s0 + 1, g = gd[w];
@@ -329,7 +329,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
             gd[w] = d0 | (d1 << 16);
         }
     } else if constexpr (C16) {
-        block_exclusive_scan16(cnt, pl.nseg, wsum);
+        block_exclusive_scan16<false, SPER>(cnt, pl.nseg, wsum);
     } else {
         block_exclusive_scan<false, SPER>(cnt, pl.nseg, wsum);
     }
