@@ -4,8 +4,10 @@
 // f64 -> u32 cast saturates), so every large filter -- config 5, any compaction output above
 // ~226M keys at p = 1e-4 -- has this m.  There 2^32 = 1 (mod m) and a bit index is hi + lo with an
 // end-around carry (mod_sat, sip13.hpp) instead of the 64-bit Barrett step.  Compiled k (4, 9, 10,
-// 19) with the length prefix (every byte key) on the 1 024-thread shape the plan picks above 2^31;
-// its own translation unit so the library still builds in parallel.
+// 19) with the length prefix (every byte key) on the 1 024-thread shape the plan picks above 2^31
+// (k = 4 also on the 512-thread shape under VBF_K1_4, an A/B that measured slower); its own
+// translation unit so the library still builds in parallel.  The runtime-k classes take the same
+// remainder in their own units (vbf_tile_pack_rk.hpp).
 #include <stdlib.h>
 
 #include "vbf_tile_pack.hpp"
