@@ -45,6 +45,7 @@ for s in $STEPS; do
     paritytest) run pytest_parity 900 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     abk14) for v in 0 1 0 1; do run bench_cfg5_k14_$v 600 env VBF_K1_4=$v python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline; grep -o '"ms_per_step": [0-9.]*\|"phases": {[^}]*}[^}]*}' "$OUT/bench_cfg5_k14_$v.log"; done ;;
     k14tests) run pytest_k14 900 env VBF_K1_4=1 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -q -m gpu -k "4294967295 or saturated or config5" --timeout 600 --timeout-method thread ;;
+    abk3cfg5) for v in 10 13 3 1 10 13; do run bench_cfg5_k3_$v 600 env VBF_K3=$v python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline --neg-keys 1000000; echo "VBF_K3=$v"; grep -o '"phases": {[^}]*}[^}]*}' "$OUT/bench_cfg5_k3_$v.log"; done ;;
     absat5) for v in 0 1 0 1; do run bench_cfg5_sat$v 600 env VBF_SAT=$v python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline; grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_cfg5_sat$v.log"; done ;;
     prof5) (cd /tmp && run prof5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5" -o run -- python3 "$ROOT/bench.py" --config 5 --steps 3 --warmup 1 --no-cpu-baseline) || exit $? ;;
     abrotl) run ab_rotl 600 env AB_LIB=velarixdb_amd/libvbf_ab.so tools/ab_lib.sh 3 ;;
