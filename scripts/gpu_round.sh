@@ -42,6 +42,7 @@ for s in $STEPS; do
     abprev5) for i in 1 2; do for lib in "" velarixdb_amd/libvbf_prev.so; do run bench_cfg5_prev$i${lib:+_prev} 600 env VBF_LIB=$lib python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline; grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_cfg5_prev$i${lib:+_prev}.log"; done; done ;;
     probe5) run bench_cfg5_probe 600 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline ;;
     probemultitests) run pytest_probe_multi 900 python -u -m pytest tests/test_gpu_probe.py tests/test_gpu_multi.py tests/test_gpu_parity.py tests/test_gpu_scale.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
+    probetests) run pytest_probe_sat 900 python -u -m pytest tests/test_gpu_probe.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     paritytest) run pytest_parity 900 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     abk14) for v in 0 1 0 1; do run bench_cfg5_k14_$v 600 env VBF_K1_4=$v python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline; grep -o '"ms_per_step": [0-9.]*\|"phases": {[^}]*}[^}]*}' "$OUT/bench_cfg5_k14_$v.log"; done ;;
     k14tests) run pytest_k14 900 env VBF_K1_4=1 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -q -m gpu -k "4294967295 or saturated or config5" --timeout 600 --timeout-method thread ;;

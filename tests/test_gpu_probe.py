@@ -19,6 +19,11 @@ CASES = [  # (L or None for var-length, len_prefix, m, k, n)
     (16, 1, 1 << 31, 10, 1_000_000),      # the largest m of the one-word remainder (fast_mod31)
     (16, 1, (1 << 31) + 1, 10, 1_000_000),  # the smallest m past it (general remainder)
     (16, 1, (1 << 31) - 1, 19, 400_000),
+    # m = 2^32 - 1 (saturated): the SAT probe packs (k = 10, 19; k = 4 above) and a runtime k
+    (16, 1, 4_294_967_295, 10, 600_000),
+    (24, 1, 4_294_967_295, 19, 300_000),
+    (None, 1, 4_294_967_295, 10, 300_000),
+    (16, 1, 4_294_967_295, 6, 400_000),
 ]
 
 
