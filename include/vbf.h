@@ -262,8 +262,25 @@ uint32_t vbf_filter_num_hash_functions(const vbf_filter* f); /* bf.rs:210-213 */
 double vbf_filter_false_positive_rate(const vbf_filter* f);  /* bf.rs:54 */
 int vbf_filter_device(const vbf_filter* f);          /* a device id or VBF_DEVICE_HOST */
 uint32_t* vbf_filter_words_dev(const vbf_filter* f); /* device pointer to the bit array (NULL if host) */
+/* Read-only device pointer to the bit array (NULL if host-resident), e.g. the source of an OR
+ * merge: unlike vbf_filter_words_dev it does not mark the bits externally written, so the host
+ * mirror stays trusted.  Readers order themselves with vbf_filter_stream_wait. */
+const uint32_t* vbf_filter_words_dev_read(const vbf_filter* f);
 /* no_of_elements = n (bf.rs:143 assigns it on recover_meta). */
 int vbf_filter_set_num_elements(vbf_filter* f, uint32_t n);
+/* Binding bookkeeping kept in the handle, so a binding's BloomFilter struct needs no private
+ * fields: velarixdb builds `BloomFilter { file_path: Some(..), ..Default::default() }` outside
+ * filter::bf (db/recovery.rs:143-146, tests/workload.rs:309-312), which a private field would
+ * forbid.  Both are per handle and copied by vbf_filter_clone, like the struct's plain fields
+ * (bf.rs:242-254).
+ * sst entries: the entry count of the SST this filter was batch-built from
+ * (build_filter_from_entries), VBF_EXT_NONE until set; the binding's write() passes it to
+ * vbf_filter_serialize_ext.  restored: vbf_filter_recover_ext loaded persisted bits;
+ * vbf_filter_take_restored returns 1 once (and clears it), so the build_filter_from_entries that
+ * follows recover_meta on the lazy-rebuild path (range.rs:117-128) can skip the rebuild. */
+int vbf_filter_set_sst_entries(vbf_filter* f, uint64_t entries);
+uint64_t vbf_filter_sst_entries(const vbf_filter* f);
+int vbf_filter_take_restored(vbf_filter* f); /* 1 or 0; < 0 on error */
 /* Move the (shared) bit array to `device` or to host memory (VBF_DEVICE_HOST), in place. */
 int vbf_filter_migrate(vbf_filter* f, int device);
 int vbf_filter_serialize(const vbf_filter* f, uint8_t out[16]); /* bf.rs:158-172 */
@@ -371,6 +388,14 @@ int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t s
 int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                          int len_prefix, uint32_t nsst, const vbf_filter* const* filters,
                          const uint8_t* bounds, const uint64_t* bounds_off, uint8_t* out);
+/* vbf_multi_probe_host's path for filters on several GPUs, with the split given: group[i] names
+ * filter i's group, each group is probed on its first filter's device (all of a group's filters
+ * must share it) and its answer columns are scattered back.  vbf_multi_probe_host calls it with
+ * group[i] = the filter's device; a one-GPU host can exercise the split with any grouping. */
+int vbf_multi_probe_host_grouped(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                                 int len_prefix, uint32_t nsst, const vbf_filter* const* filters,
+                                 const uint8_t* bounds, const uint64_t* bounds_off, const int* group,
+                                 uint8_t* out);
 
 /* ---- compaction merge ----
  * One bucket of SizedTierRunner::merge_ssts_in_buckets (src/compactors/sized.rs:170-200): the

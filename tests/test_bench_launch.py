@@ -59,6 +59,20 @@ def test_two_rank_spawn_gets_config4_shards():
         assert x["seed"] == 0x5EED0040 + x["rank"]
 
 
+def test_eight_rank_spawn_gets_config4_shards():
+    """The driver's 8-GPU scaling run, rehearsed on CPU: `bench.py --gpus 8` with no launcher
+    starts 8 ranks in one process group, each on its own local rank, rank r on config 4's shard r
+    (seed 0x5EED0040 + r) -- one merged table's filter per GPU (compactors/sized.rs:170-200)."""
+    r = _plan(["--gpus", "8"])
+    assert r["world_size"] == 8 and r["n_gpus"] == 8
+    assert [x["rank"] for x in r["ranks"]] == list(range(8))
+    assert sorted(x["local_rank"] for x in r["ranks"]) == list(range(8))
+    for x in r["ranks"]:
+        assert (x["config"], x["keys"], x["m"], x["k"]) == (4, 50_000_000, 500_000_000, 10)
+        assert x["seed"] == 0x5EED0040 + x["rank"]
+    assert len({x["seed"] for x in r["ranks"]}) == 8
+
+
 def test_one_gpu_default_is_config2():
     r = _plan([])
     assert r["world_size"] == 1

@@ -1,4 +1,4 @@
-"""world_size-2 (and 3) gloo runs of the multi-GPU exchange (velarixdb_amd/dist.py) on CPU.
+"""world_size-2, 3 and 8 gloo runs of the multi-GPU exchange (velarixdb_amd/dist.py) on CPU.
 
 The partial filters here are built by the oracle (the checker) from each rank's key shard; the
 property under test is the exchange: OR-all-reduce(partials) == the filter of all keys
@@ -42,8 +42,10 @@ def _worker(rank, world, port, m, k, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_or_allreduce_equals_single_filter(world, ora):
+    """world 8 is the target node's rank count: 31 251 words split into
+    8 chunks of 3 907 with 5 padding words, as config 5's exchange does at full size."""
     from velarixdb_amd.keys import HostBatch
     m, k, n = 1_000_003, 4, 40_000  # nwords not divisible by world: exercises the padding
     ctx = mp.get_context("spawn")

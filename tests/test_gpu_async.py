@@ -398,3 +398,78 @@ def test_async_set_failure_reported_by_next_call(vbf, ora):
     with pytest.raises(VbfError):
         f.contains_batch(HostBatch(host[:L], None, L, 1, 1))
     assert f.contains_batch(HostBatch(host[:L], None, L, 1, 1)).all()
+
+
+def test_fork_with_a_queued_set_fails_fast_in_the_child(vbf, ora):
+    """a child forked while the parent has a set queued on a filter makes
+    set_host_async its first call on that filter.  The parent's job never runs in the child, so
+    the call must return VBF_EINVAL (AssertionError in the binding) at once instead of queueing
+    behind it and leaving every later drain waiting forever; the child's copy of the binding's
+    in-flight table is empty (no 60 s wait at exit).  The child makes no HIP call.  The parent's
+    jobs are held in the device's worker by a release callback that blocks until the fork is over,
+    so the set is deterministically still queued; afterwards the parent's words equal the oracle's."""
+    import os
+    from velarixdb_amd import filter as vf
+    from velarixdb_amd._lib import call
+    from velarixdb_amd.keys import HostBatch
+    n, L = 200_000, 16
+    gate = threading.Event()
+    CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    cb = CB(lambda ctx: gate.wait(60))
+    fa = vbf.BloomFilter(0.01, n)
+    fb = vbf.BloomFilter(0.01, n, device=fa.device)
+    ha = ora.gen_fixed(0x5EED0E40, 0, n, L)
+    hb = ora.gen_fixed(0x5EED0E41, 0, n, L)
+    # fa's job runs, then the worker blocks in its release callback: fb's job stays queued
+    call("vbf_filter_set_host_async", fa._h, ha.ctypes.data, None, L, n, 1, ctypes.cast(cb, ctypes.c_void_p), 1)
+    fb.set_many_async(HostBatch(hb, None, L, n, 1), zero_copy=True)
+    assert vf._INFLIGHT and fb.busy()
+    pid = os.fork()
+    if pid == 0:  # the child: no HIP call on any path below
+        code = 3
+        try:
+            try:
+                fb.set_many_async(HostBatch(hb[:L * 10], None, L, 10, 1))
+                code = 1  # queued behind a job that never runs here
+            except AssertionError as e:
+                code = 0 if "forked" in str(e) else 2
+            if vf._INFLIGHT:
+                code = 4
+        finally:
+            os._exit(code)
+    try:
+        _, status = os.waitpid(pid, 0)
+    finally:
+        gate.set()
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status
+    fb.sync()
+    fa.sync()
+    assert np.array_equal(fb.words(), _oracle_words(ora, 0x5EED0E41, n, fb.num_bits(), fb.no_of_hash_func))
+    assert np.array_equal(fa.words(), _oracle_words(ora, 0x5EED0E40, n, fa.num_bits(), fa.no_of_hash_func))
+
+
+def test_words_dev_read_keeps_the_mirror(vbf, ora):
+    """the read-only pointer (vbf_filter_words_dev_read, the OR source of a
+    merge) does not mark the filter externally written, so single-key contains keep answering
+    from the host mirror -- while vbf_filter_words_dev does mark it (every host read copies)."""
+    from velarixdb_amd.keys import HostBatch
+    n, L = 100_000, 16
+    h = ora.gen_fixed(0x5EED0E50, 0, n, L)
+    f = vbf.BloomFilter(0.01, n)
+    f.set_batch(HostBatch(h, None, L, n, 1))
+    assert f.contains(bytes(h[:L]))
+    ro = f.words_dev_read_ptr()
+    assert ro and ro == f.words_dev_read_ptr()
+    # a device write behind the library's back is NOT seen through the mirror after a read-only
+    # hand-out (by contract the reader does not write) ...
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    neg = ora.gen_fixed(0x5EED0E51, 0, 64, L)
+    assert not f.contains_batch(HostBatch(neg, None, L, 64, 1)).all()
+    vbf._lib.call("vbf_build_dev", ctypes.c_void_p(torch.from_numpy(neg).to("cuda:0").data_ptr()), None, L, 64, 1,
+                  f.num_bits(), f.no_of_hash_func, ctypes.c_void_p(ro), ctypes.c_void_p(s.cuda_stream))
+    s.synchronize()
+    assert not f.contains_batch(HostBatch(neg, None, L, 64, 1)).all()  # the mirror was trusted
+    # ... while the writable pointer makes every host read copy the words again
+    f.words_dev_ptr()
+    assert f.contains_batch(HostBatch(neg, None, L, 64, 1)).all()

@@ -296,3 +296,38 @@ def test_group_pipeline_edge_sizes(vbf, ora, multi_mode, m, k):
     for s_ in range(S):
         want = ora.probe(hb, m, k, words[s_], threads=8)[sl].astype(bool)
         assert np.array_equal(outs["1"][sl, s_].astype(bool), want), s_
+
+
+@pytest.mark.parametrize("groups", [[0, 1, 0, 2, 1, 0], [5, 4, 3, 2, 1, 0], [7, 7, 7, 7, 7, 7]])
+def test_grouped_split_equals_one_device_probe(vbf, ora, groups):
+    """the path vbf_multi_probe_host takes for filters on several GPUs -- split
+    per device, bound bytes re-based per group, keys staged to each, answer columns scattered back
+    -- run on this one GPU with the split given (vbf_multi_probe_host_grouped), ranged bounds and
+    variable-length keys: equal to the single-device probe and to the oracle."""
+    from velarixdb_amd._lib import call
+    from velarixdb_amd.key_range import SstRange, _bounds, candidates
+    from velarixdb_amd.keys import pack
+    rng = np.random.default_rng(sum(groups))
+    specs = [(0.01, 5000), (0.1, 800), (1e-4, 3000), (0.3, 20000), (1.0, 5), (1e-3, 7000)]
+    ranges, orc = [], []
+    for p, n in specs:
+        f = vbf.BloomFilter(p, n)
+        ks = sorted(rng.bytes(int(rng.integers(1, 30))) for _ in range(n))
+        f.set_many(ks)
+        lo, hi = ks[len(ks) // 5], ks[4 * len(ks) // 5]
+        ranges.append(SstRange(lo, hi, f))
+        orc.append((lo, hi, f.num_bits(), f.no_of_hash_func, ora.build_words(pack(ks), f.num_bits(), f.no_of_hash_func)))
+    q = [rng.bytes(int(rng.integers(0, 40))) for _ in range(3000)] + [r.smallest_key for r in ranges] + \
+        [r.biggest_key for r in ranges]
+    b = pack(q)
+    raw, offs = _bounds(ranges)
+    handles = (ctypes.c_void_p * len(ranges))(*[r.filter._h.value for r in ranges])
+    grp = (ctypes.c_int * len(ranges))(*groups)
+    out = np.zeros((b.n, len(ranges)), np.uint8)
+    d, o = b.ptrs()
+    call("vbf_multi_probe_host_grouped", d, o, b.stride, b.n, b.len_prefix, len(ranges), handles, raw.ctypes.data,
+         offs.ctypes.data, grp, out.ctypes.data)
+    assert np.array_equal(out.astype(bool), candidates(q, ranges))
+    for s, (lo, hi, m, k, words) in enumerate(orc):
+        inr = np.array([lo <= x <= hi for x in q])
+        assert np.array_equal(out[:, s].astype(bool), inr & _oracle_contains(ora, q, m, k, words)), s

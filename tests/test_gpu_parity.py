@@ -562,6 +562,106 @@ def test_partitioned_build_knobs_same_words(vbf, ora, tmp_path):
                 assert np.array_equal(got, want[(m, k)]), (k1, et, k3, sp, m, k)
 
 
+# (m, k, layout) the kernel-selecting knobs gate: m = 2^32 - 1 (SAT / Barrett, k = 4 / 6 / 10 / 19,
+# fixed and runtime-length keys), the runtime-k classes (k = 7, 14, 23), k = 19 and 10 on the 512-
+# and 1 024-thread shapes; `probe`: the partitioned probe is also run (round-3 pipeline: VBF_Q3)
+KNOB_CASES = (
+    (4_294_967_295, 4, "f32", True), (4_294_967_295, 4, "f16", True), (4_294_967_295, 6, "f16", True),
+    (4_294_967_295, 10, "f16", False), (4_294_967_295, 19, "f16", True), (4_294_967_295, 4, "var", True),
+    (4_294_967_295, 7, "var", False), (20_000_003, 7, "f16", True), (30_000_001, 14, "var", False),
+    (40_000_000, 23, "f32", False), (3_800_017, 19, "f16", False), (10_000_000, 10, "var", False),
+    (6_000_011, 10, "f16", True),
+)
+# every kernel-changing knob of DESIGN.md section 8b that VERDICT r04 found untested (one child each;
+# the library reads them once per process)
+KNOB_COMBOS = (
+    {"VBF_SAT": "0"}, {"VBF_KCLASS": "0"}, {"VBF_K1_4": "1"}, {"VBF_C16": "0"}, {"VBF_C16": "1"},
+    {"VBF_C16": "1", "VBF_K1": "0"}, {"VBF_Q3": "0"}, {},
+)
+
+
+def test_kernel_knobs_same_words(vbf, ora, tmp_path):
+    """the speed-only knobs that select other kernels -- VBF_SAT=0 (the
+    Barrett kernels at m = 2^32 - 1), VBF_KCLASS=0 (the scratch-stash runtime-k kernel), VBF_K1_4=1
+    (k = 4 on the 512-thread shape: the case whose packed-counter scan was once wrong),
+    VBF_C16=0/1 (plain or packed segment counters, on either K1 shape), VBF_Q3=0 (the partitioned
+    probe's one-pass segment test) -- give the oracle's words (bf.rs:84-92) and probe answers
+    (bf.rs:95-105) at the shapes they gate.  Each setting runs in a child process; the parent
+    compares every child's words and answers with the oracle's."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    from velarixdb_amd.keys import pack_fixed, pack_offsets
+    from velarixdb_amd.workloads import SEED_CFG3, var_offsets
+    n = 300_000
+    f16 = ora.gen_fixed(0x5EED0A16, 0, n, 16).reshape(n, 16)
+    f32 = ora.gen_fixed(0x5EED0A32, 0, n, 32).reshape(n, 32)
+    vo = var_offsets(SEED_CFG3, 11, n)
+    vd = ora.gen_var(SEED_CFG3, 11, vo)
+    # probe batches: the first half of the keys (positives) + as many negatives
+    nf16 = ora.gen_fixed(0x5EED0B16, 0, n // 2, 16).reshape(-1, 16)
+    nf32 = ora.gen_fixed(0x5EED0B32, 0, n // 2, 32).reshape(-1, 32)
+    nvo = var_offsets(SEED_CFG3 ^ 0xFF, 5, n // 2)
+    nvd = ora.gen_var(SEED_CFG3 ^ 0xFF, 5, nvo)
+    h = int(vo[n // 2])
+    pvd = np.concatenate([vd[:h], nvd])
+    pvo = np.concatenate([vo[: n // 2 + 1], nvo[1:] + np.uint64(h)])
+    arrs = dict(f16=f16, f32=f32, vd=vd, vo=vo, pf16=np.concatenate([f16[: n // 2], nf16]),
+                pf32=np.concatenate([f32[: n // 2], nf32]), pvd=pvd, pvo=pvo)
+    np.savez(tmp_path / "keys.npz", **arrs)
+    batches = {"f16": pack_fixed(f16), "f32": pack_fixed(f32), "var": pack_offsets(vd, vo)}
+    pbatches = {"f16": pack_fixed(arrs["pf16"]), "f32": pack_fixed(arrs["pf32"]), "var": pack_offsets(pvd, pvo)}
+    code = (
+        "import sys, ctypes; sys.path.insert(0, %r)\n"
+        "import numpy as np, torch, velarixdb_amd as v\n"
+        "from velarixdb_amd.keys import pack_fixed, pack_offsets\n"
+        "a = np.load(sys.argv[2])\n"
+        "B = {'f16': pack_fixed(a['f16']), 'f32': pack_fixed(a['f32']), 'var': pack_offsets(a['vd'], a['vo'])}\n"
+        "P = {'f16': pack_fixed(a['pf16']), 'f32': pack_fixed(a['pf32']), 'var': pack_offsets(a['pvd'], a['pvo'])}\n"
+        "vp = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None\n"
+        "res = {}\n"
+        "for i, (m, k, lay, probe) in enumerate(%r):\n"
+        "    b = B[lay]\n"
+        "    w = np.zeros((m + 31) // 32, np.uint32)\n"
+        "    d, o = b.ptrs()\n"
+        "    v._lib.call('vbf_build_host', d, o, b.stride, b.n, 1, m, k, w.ctypes.data, w.size, 0)\n"
+        "    nz = np.flatnonzero(w)\n"
+        "    res['nz%%d' %% i], res['w%%d' %% i] = nz.astype(np.uint64), w[nz]\n"
+        "    if probe:\n"
+        "        pb = P[lay]\n"
+        "        kd = torch.from_numpy(pb.data).cuda()\n"
+        "        od = torch.from_numpy(pb.offsets.view(np.int64)).cuda() if pb.offsets is not None else None\n"
+        "        wd = torch.from_numpy(w.view(np.int32)).cuda()\n"
+        "        out = torch.zeros(pb.n, dtype=torch.uint8, device='cuda')\n"
+        "        v._lib.call('vbf_probe_dev_ex', vp(kd), vp(od), pb.stride, pb.n, 1, m, k, vp(wd), vp(out), 2, None)\n"
+        "        torch.cuda.synchronize()\n"
+        "        res['p%%d' %% i] = out.cpu().numpy()\n"
+        "        del kd, od, wd, out\n"
+        "np.savez(sys.argv[1], **res)\n"
+        "print('ok')\n" % (ROOT, KNOB_CASES))
+    outs = []
+    for j, knobs in enumerate(KNOB_COMBOS):
+        env = {kk: vv for kk, vv in os.environ.items() if kk != "VBF_LIB" and not kk.startswith("VBF_")}
+        env.update(knobs)
+        stem = str(tmp_path / ("knob%d.npz" % j))
+        r = subprocess.run([sys.executable, "-c", code, stem, str(tmp_path / "keys.npz")], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "ok" in r.stdout, (knobs, r.stderr[-2000:])
+        outs.append(stem)
+    for i, (m, k, lay, probe) in enumerate(KNOB_CASES):
+        want = ora.build_words(batches[lay], m, k, threads=8)
+        wp = ora.probe(pbatches[lay], m, k, want, threads=8) if probe else None
+        for j, knobs in enumerate(KNOB_COMBOS):
+            res = np.load(outs[j])
+            nz, val = res["nz%d" % i], res["w%d" % i]
+            wnz = np.flatnonzero(want)
+            assert np.array_equal(nz, wnz.astype(np.uint64)) and np.array_equal(val, want[wnz]), (knobs, m, k, lay)
+            if probe:
+                assert np.array_equal(res["p%d" % i], wp), (knobs, m, k, lay)
+        if probe:
+            assert wp[: n // 2].all()  # no false negative
+
+
 @pytest.mark.parametrize("strategy", [1, 2])
 def test_concentrated_indices(vbf, ora, strategy):
     """Adversarial skew: 3M copies of three keys put every tile's 30K bit indices into a handful of

@@ -247,24 +247,6 @@ def test_config3_full_size_bit_exact(vbf, ora):
     assert abs(fp / nn - fill ** k) < 5e-4
 
 
-def test_config5_sizing_slice(vbf, ora):
-    """Config 5's saturated m (2^32-1 bits, k = 4) on 200M x 32 B keys (a 1/5 slice)."""
-    from velarixdb_amd.workloads import SEED_CFG5, fpr_for_bits_per_key
-    N = 1_000_000_000
-    m = vbf.num_bits(N, fpr_for_bits_per_key(15))
-    k = vbf.num_hash_functions(m, N)
-    assert (m, k) == (4294967295, 4)
-    n, L = 200_000_000, 32
-    keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
-    vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG5, 0, n, L, vp(keys), sp())
-    w_part = build(vbf, keys, None, L, n, m, k, 2)
-    w_atom = build(vbf, keys, None, L, n, m, k, 1)
-    assert torch.equal(w_part, w_atom)
-    assert count(vbf, keys, None, L, n, m, k, w_part) == n
-    fill = popcount(vbf, w_part) / m
-    assert abs(fill - (1 - math.exp(-k * n / m))) < 1e-3
-
-
 def test_multi_chunk_partitioned_paths(vbf):
     """More bit indices in one call than one chunk holds (build: kBuildChunkIdx = 2^31, probe:
     kPartChunkIdx = 2^30): both partitioned paths process the batch in chunks.  The chunked

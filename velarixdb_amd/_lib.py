@@ -86,6 +86,10 @@ SIGNATURES = {
     "vbf_filter_false_positive_rate": (_dbl, [_vp]),
     "vbf_filter_device": (_int, [_vp]),
     "vbf_filter_words_dev": (_vp, [_vp]),
+    "vbf_filter_words_dev_read": (_vp, [_vp]),
+    "vbf_filter_set_sst_entries": (_int, [_vp, _u64]),
+    "vbf_filter_sst_entries": (_u64, [_vp]),
+    "vbf_filter_take_restored": (_int, [_vp]),
     "vbf_filter_set_num_elements": (_int, [_vp, _u32]),
     "vbf_filter_migrate": (_int, [_vp, _int]),
     "vbf_filter_serialize": (_int, [_vp, _vp]),
@@ -95,6 +99,7 @@ SIGNATURES = {
     "vbf_gen_sst_fixed_dev": (_int, [_u64, _u64, _u64, _u32, _vp, _vp, _vp]),
     "vbf_multi_probe_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp, _vp, _vp, _vp]),
     "vbf_multi_probe_host": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp, _vp, _vp]),
+    "vbf_multi_probe_host_grouped": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp, _vp, _vp, _vp]),
     "vbf_compact_merge_dev": (_int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _u64, _int, _u64, _u64, _u64,
                                       _vp, _vp, _vp, _vp, _vp, _vp]),
     "vbf_compact_merge_host": (_int, [_vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _u64, _int, _u64, _u64, _u64,

@@ -62,7 +62,7 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     return out
 
 
-EXAMPLES = ("c_host", "memtable_latency")
+EXAMPLES = ("c_host", "memtable_latency", "rust_replay")
 
 
 def build_examples(verbose=False):

@@ -1093,6 +1093,12 @@ struct vbf_filter {
     uint32_t k = 0;
     std::atomic<uint32_t> n{0};
     double p = 0.0;
+    // Binding bookkeeping that lives in the handle, so a binding's BloomFilter needs no private
+    // fields (velarixdb builds `BloomFilter { file_path, ..Default::default() }` outside
+    // filter::bf: db/recovery.rs:143-146, tests/workload.rs:309-312).  Per handle, copied by clone
+    // like the struct's other plain fields (bf.rs:242-254).
+    std::atomic<uint64_t> sst_entries{VBF_EXT_NONE};  // the SST's entry count (build_filter_from_entries)
+    std::atomic<int> restored{0};  // vbf_filter_recover_ext loaded persisted bits (not yet taken)
 };
 
 extern "C" {
@@ -1451,6 +1457,8 @@ int vbf_filter_clone(const vbf_filter* f, vbf_filter** out) {
     c->k = f->k;
     c->n.store(f->n.load());  // bf.rs:248: the clone's counter is a copy, the bits are shared
     c->p = f->p;
+    c->sst_entries.store(f->sst_entries.load());
+    c->restored.store(f->restored.load());
     *out = c;
     return ok();
 }
@@ -1480,10 +1488,28 @@ uint32_t* vbf_filter_words_dev(const vbf_filter* f) {
     return s.d_words;
 }
 
+const uint32_t* vbf_filter_words_dev_read(const vbf_filter* f) {
+    if (!f) return nullptr;
+    Storage& s = *f->bits;
+    std::lock_guard<std::mutex> lk(s.mu);
+    return s.d_words;  // read-only use: the mirror and `pristine` stay trusted
+}
+
 int vbf_filter_set_num_elements(vbf_filter* f, uint32_t n) {
     if (!f) return fail(VBF_EINVAL, "filter is NULL");
     f->n.store(n);
     return ok();
+}
+
+int vbf_filter_set_sst_entries(vbf_filter* f, uint64_t entries) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    f->sst_entries.store(entries);
+    return ok();
+}
+uint64_t vbf_filter_sst_entries(const vbf_filter* f) { return f ? f->sst_entries.load() : VBF_EXT_NONE; }
+int vbf_filter_take_restored(vbf_filter* f) {
+    if (!f) return fail(VBF_EINVAL, "filter is NULL");
+    return f->restored.exchange(0);
 }
 
 int vbf_filter_serialize(const vbf_filter* f, uint8_t out[16]) {
@@ -1583,6 +1609,14 @@ int vbf_filter_set_host_async(vbf_filter* f, const uint8_t* keys, const uint64_t
         lk.unlock();
         if (release) release(release_ctx);
     } else {
+        if (s.jobs_pid != getpid() && s.jobs_done != s.jobs_queued) {
+            // forked while the parent had sets queued on this filter: they never run here.  Report
+            // that now (as every other call does) instead of overwriting jobs_pid, which would make
+            // the parent's jobs look like this process's and every later drain wait forever
+            // (ADVICE r04).  The caller keeps its buffers: release is not called on an error.
+            (void)storage_jobs_settled(s);
+            if ((rc = storage_drain(s, lk))) return rc;
+        }
         ++s.jobs_queued;
         s.jobs_pid = getpid();
         s.pristine = false;
@@ -1980,6 +2014,7 @@ int vbf_filter_recover_ext(const uint8_t* bytes, uint64_t len, int device, vbf_f
                 }
                 // recover_meta + build_filter_from_entries (range.rs:121-124): stored n + entries
                 f->n.store((uint32_t)(f->n.load() + get_u64(e + 16)));
+                f->restored.store(1);
                 if (restored) *restored = 1;
             }
         }
@@ -2411,6 +2446,52 @@ int multi_probe_host_device(const uint8_t* keys, const uint64_t* offsets, uint64
     HIP_TRY(hipStreamSynchronize(s));
     return VBF_OK;
 }
+
+// vbf_multi_probe_host over filters split into groups (group[i] of filter i; the multi-device
+// path groups by device): each group is probed on the device of its first filter, with the keys
+// staged there, its filters' bound bytes re-based into a bounds array of their own, and its answer
+// columns scattered back into out[n][nsst].  Caller holds every filter's lock (drained).
+int multi_probe_host_groups(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                            int len_prefix, uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
+                            const uint64_t* bounds_off, uint8_t* out, const int* group) {
+    std::vector<int> gs;
+    for (uint32_t i = 0; i < nsst; ++i)
+        if (std::find(gs.begin(), gs.end(), group[i]) == gs.end()) gs.push_back(group[i]);
+    std::vector<const vbf_filter*> sub;
+    std::vector<uint32_t> cols;
+    std::vector<uint8_t> sb, tmp;
+    std::vector<uint64_t> so;
+    for (const int g : gs) {
+        sub.clear();
+        cols.clear();
+        sb.clear();
+        so.assign(1, 0);
+        for (uint32_t i = 0; i < nsst; ++i) {
+            if (group[i] != g) continue;
+            sub.push_back(filters[i]);
+            cols.push_back(i);
+            if (bounds_off) {  // this filter's [lo, hi) bound bytes, re-based
+                sb.insert(sb.end(), bounds + bounds_off[2 * i], bounds + bounds_off[2 * i + 1]);
+                so.push_back(sb.size());
+                sb.insert(sb.end(), bounds + bounds_off[2 * i + 1], bounds + bounds_off[2 * i + 2]);
+                so.push_back(sb.size());
+            }
+        }
+        const uint32_t ns = (uint32_t)sub.size();
+        const int dev = sub[0]->bits->device;
+        for (const vbf_filter* f : sub)
+            if (f->bits->device != dev)
+                return fail(VBF_EINVAL, "a group's filters live on devices %d and %d", dev, f->bits->device);
+        tmp.resize(n * ns);
+        if (int rc = multi_probe_host_device(keys, offsets, stride, n, len_prefix, ns, sub.data(),
+                                             bounds_off ? sb.data() : nullptr, bounds_off ? so.data() : nullptr,
+                                             tmp.data(), dev))
+            return rc;
+        for (uint64_t j = 0; j < n; ++j)
+            for (uint32_t q = 0; q < ns; ++q) out[j * nsst + cols[q]] = tmp[j * ns + q];
+    }
+    return VBF_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -2455,37 +2536,36 @@ int vbf_multi_probe_host(const uint8_t* keys, const uint64_t* offsets, uint64_t 
             return rc;
         return ok();
     }
-    // filters on several GPUs: each device probes its own filters (the keys are staged to each),
-    // and its answer columns are scattered into out[n][nsst]
-    std::vector<const vbf_filter*> sub;
-    std::vector<uint32_t> cols;
-    std::vector<uint8_t> sb, tmp;
-    std::vector<uint64_t> so;
-    for (const int d : devices) {
-        sub.clear();
-        cols.clear();
-        sb.clear();
-        so.assign(1, 0);
-        for (uint32_t i = 0; i < nsst; ++i) {
-            if (filters[i]->bits->device != d) continue;
-            sub.push_back(filters[i]);
-            cols.push_back(i);
-            if (bounds_off) {  // this filter's [lo, hi) bound bytes, re-based
-                sb.insert(sb.end(), bounds + bounds_off[2 * i], bounds + bounds_off[2 * i + 1]);
-                so.push_back(sb.size());
-                sb.insert(sb.end(), bounds + bounds_off[2 * i + 1], bounds + bounds_off[2 * i + 2]);
-                so.push_back(sb.size());
-            }
-        }
-        const uint32_t ns = (uint32_t)sub.size();
-        tmp.resize(n * ns);
-        if ((rc = multi_probe_host_device(keys, offsets, stride, n, len_prefix, ns, sub.data(),
-                                          bounds_off ? sb.data() : nullptr, bounds_off ? so.data() : nullptr,
-                                          tmp.data(), d)))
-            return rc;
-        for (uint64_t j = 0; j < n; ++j)
-            for (uint32_t q = 0; q < ns; ++q) out[j * nsst + cols[q]] = tmp[j * ns + q];
+    // filters on several GPUs: each device probes its own filters
+    std::vector<int> group(nsst);
+    for (uint32_t i = 0; i < nsst; ++i) group[i] = filters[i]->bits->device;
+    if ((rc = multi_probe_host_groups(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out,
+                                      group.data())))
+        return rc;
+    return ok();
+}
+
+int vbf_multi_probe_host_grouped(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
+                                 int len_prefix, uint32_t nsst, const vbf_filter* const* filters,
+                                 const uint8_t* bounds, const uint64_t* bounds_off, const int* group, uint8_t* out) {
+    int rc = check_keys(keys, offsets, stride, n);
+    if (rc) return rc;
+    if (!nsst || !n) return ok();
+    if (!filters || !group || !out) return fail(VBF_EINVAL, "NULL argument");
+    for (uint32_t i = 0; i < nsst; ++i)
+        if (!filters[i]) return fail(VBF_EINVAL, "filters[%u] is NULL", i);
+    if (bounds_off) {
+        for (uint32_t i = 0; i < 2 * nsst; ++i)
+            if (bounds_off[i + 1] < bounds_off[i]) return fail(VBF_EINVAL, "bounds_off not nondecreasing at %u", i);
+        if (bounds_off[2 * nsst] && !bounds) return fail(VBF_EINVAL, "bounds is NULL");
     }
+    MultiLock lk(filters, nsst);
+    if ((rc = lk.drain())) return rc;
+    for (uint32_t i = 0; i < nsst; ++i)
+        if (filters[i]->bits->host()) return host_resident("vbf_multi_probe_host_grouped");
+    if ((rc = multi_probe_host_groups(keys, offsets, stride, n, len_prefix, nsst, filters, bounds, bounds_off, out,
+                                      group)))
+        return rc;
     return ok();
 }
 

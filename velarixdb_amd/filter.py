@@ -73,6 +73,12 @@ def _release(ctx):
 
 _RELEASE_PTR = ctypes.cast(_release, ctypes.c_void_p)
 
+# A forked child inherits _INFLIGHT, but the jobs behind those entries never run there (the
+# library reports them as failed, vbf.h), so nothing would ever release them: the child forgets
+# them instead of waiting 60 s for them at exit.
+if hasattr(os, "register_at_fork"):
+    os.register_at_fork(after_in_child=_INFLIGHT.clear)
+
 
 @__import__("atexit").register
 def _drain_inflight():
@@ -171,6 +177,23 @@ class BloomFilter:
         call("vbf_filter_migrate", self._h, _dev(device))
         return self
 
+    def set_sst_entries(self, n):
+        """Record the entry count of the SST this filter was built from (handle bookkeeping that
+        the Rust binding's write() hands to serialize_ext; vbf_filter_set_sst_entries)."""
+        call("vbf_filter_set_sst_entries", self._h, VBF_EXT_NONE if n is None else int(n))
+
+    @property
+    def sst_entries(self):
+        v = int(lib.vbf_filter_sst_entries(self._h))
+        return None if v == VBF_EXT_NONE else v
+
+    def take_restored(self):
+        """True once after recover_meta() loaded persisted bits (vbf_filter_take_restored)."""
+        rc = lib.vbf_filter_take_restored(self._h)
+        if rc < 0:
+            _lib.check("vbf_filter_take_restored", rc)
+        return bool(rc)
+
     def set_num_elements(self, n):
         """bf.rs:143: `self.no_of_elements = AtomicU32::new(n)`."""
         call("vbf_filter_set_num_elements", self._h, int(n) & 0xFFFFFFFF)
@@ -188,7 +211,12 @@ class BloomFilter:
         return (self.num_bits() + 31) // 32
 
     def words_dev_ptr(self):
+        """Device pointer for a caller that WRITES the bits (declare it with stream_record)."""
         return lib.vbf_filter_words_dev(self._h)
+
+    def words_dev_read_ptr(self):
+        """Device pointer for read-only use (the host mirror stays trusted)."""
+        return lib.vbf_filter_words_dev_read(self._h)
 
     def get_sst_dir(self):
         if self.sst_dir is None:
