@@ -36,7 +36,11 @@ __global__ void k_gen(uint32_t* bnd, uint32_t ntiles, uint32_t nseg, uint32_t me
 // (run, group index) into a per-wave LDS slot table and the group lanes read their slot -- one LDS
 // write per group and one read instead of the 6-step binary search over the prefix (ds_bpermute)
 // plus two shuffles
-template <int GE, int GB, bool LOC = false>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// NT (g20 only, round 5): the group loads as non-temporal loads (global_load ... nt), to see
+// whether the L1 then stops filling whole 128-byte lines for the ~20 useful bytes of a short run
+template <int GE, int GB, bool LOC = false, bool NT = false>
 __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles,
                                                uint32_t nseg, uint32_t tile_bytes, uint32_t* out) {
     extern __shared__ uint32_t lds[];
@@ -88,6 +92,10 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
             } else if (GB == 16) {
                 l = *reinterpret_cast<const uint4*>(tile + gi * 16);
                 acc ^= l.x ^ l.y ^ l.z ^ l.w;
+            } else if (NT) {
+                const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(tile + gi * GB));
+                const uint32_t nb = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(tile + gi * GB + 16));
+                acc ^= v4.x ^ v4.y ^ v4.z ^ v4.w ^ nb;
             } else {
                 uint32_t nb;
                 __builtin_memcpy(&l, tile + gi * GB, 16);
@@ -101,19 +109,19 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
     if (threadIdx.x == 0 && lds[0] == 0x12345678u) out[0] = acc;
 }
 
-template <int GE, int GB, bool LOC = false>
+template <int GE, int GB, bool LOC = false, bool NT = false>
 static float run(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles, uint32_t nseg, uint32_t tile_bytes,
                  uint32_t* out) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     const uint32_t lds = 128 * 1024 + 16 * 512 * 4;  // bitmap + per-wave slot tables (LOC)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_read<GE, GB, LOC>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_read<GE, GB, LOC, NT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL((k_read<GE, GB, LOC>), dim3(nseg), dim3(1024), lds, 0, img, bnd, ntiles, nseg, tile_bytes, out);
+    hipLaunchKernelGGL((k_read<GE, GB, LOC, NT>), dim3(nseg), dim3(1024), lds, 0, img, bnd, ntiles, nseg, tile_bytes, out);
     (void)hipEventRecord(e0);
     for (int r = 0; r < 5; ++r)
-        hipLaunchKernelGGL((k_read<GE, GB, LOC>), dim3(nseg), dim3(1024), lds, 0, img, bnd, ntiles, nseg, tile_bytes,
+        hipLaunchKernelGGL((k_read<GE, GB, LOC, NT>), dim3(nseg), dim3(1024), lds, 0, img, bnd, ntiles, nseg, tile_bytes,
                            out);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
@@ -135,7 +143,7 @@ int main() {
         hipLaunchKernelGGL(k_gen, dim3((c.ntiles + 255) / 256), dim3(256), 0, 0, bnd, c.ntiles, c.nseg, c.mean, used);
         uint32_t cap = 0;
         (void)hipMemcpy(&cap, used, 4, hipMemcpyDeviceToHost);
-        for (int fmt : {0, 3}) {
+        for (int fmt : {0, 4}) {
             const uint32_t tile_bytes = fmt != 1 ? ((cap + 7) / 8 * 20 + 16 + 15) & ~15u : ((cap + 5) / 6 * 16 + 16);
             const uint64_t bytes = (uint64_t)c.ntiles * tile_bytes + 4096;
             uint8_t* img;
@@ -145,9 +153,10 @@ int main() {
                 const float ms = fmt == 0   ? run<8, 20>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
                                  : fmt == 1 ? run<6, 16>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
                                  : fmt == 3 ? run<8, 20, true>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
+                                 : fmt == 4 ? run<8, 20, false, true>(img, bnd, c.ntiles, c.nseg, tile_bytes, out)
                                             : run<8, 0>(img, bnd, c.ntiles, c.nseg, tile_bytes, out);
                 printf("%-6s %s %.3f ms  (%.1f G runs/s, %u B per tile, %.2f GB image)\n", c.name,
-                       fmt == 0 ? "g20" : fmt == 1 ? "g16" : fmt == 3 ? "g20loc" : "raw20", ms,
+                       fmt == 0 ? "g20" : fmt == 1 ? "g16" : fmt == 3 ? "g20loc" : fmt == 4 ? "g20nt" : "raw20", ms,
                        (double)nb / (ms * 1e-3) / 1e9, tile_bytes,
                        (double)c.ntiles * tile_bytes / 1e9);
             }

@@ -665,6 +665,15 @@ hipError_t launch_group_pack(const KeyBatch& kb, const DevKeys& dk, const PartPl
     return err;
 }
 
+hipError_t launch_tile_pack_main(int fmt, bool lp, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                 uint32_t* tiles, uint16_t* ends, hipStream_t s) {
+    switch (fmt) {
+        case 16: case 32: return launch_tile_pack_main_a(fmt, lp, dk, pl, ntiles, tiles, ends, s);
+        case 8: case 24: return launch_tile_pack_main_b(fmt, lp, dk, pl, ntiles, tiles, ends, s);
+        default: return launch_tile_pack_main_c(fmt, lp, dk, pl, ntiles, tiles, ends, s);
+    }
+}
+
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
                                     void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s, bool fresh) {
     if (kb.n == 0 || k == 0) return hipSuccess;
@@ -698,37 +707,10 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                    (err = launch_tile_pack_sat(pick_fmt(dk.keys, dk.offsets, dk.stride), dk, pl, ntiles, tiles,
                                                pl.ends_t ? endsT : ends, s)) != hipErrorNotSupported) {
             // m = 2^32 - 1 (the reference's saturated size): end-around-carry remainders (SAT kernels)
-        } else with_fmt(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, [&]<int FMT, bool LP>() {
-            err = hipSuccess;
-            // m <= 2^31: the one-word remainder (fast_mod31); the runtime-k kernel keeps the general one
-            auto pick = [&]<bool S>() {
-                if constexpr (FMT > 0 && S) {  // the 512-thread shape (make_plan: m <= 2^31)
-                    if (pl.k1v && k == 10) return pl.c16 ? k_tile_pack<FMT, LP, 10, true, true, 1>
-                                                         : k_tile_pack<FMT, LP, 10, true, false, 1>;
-                    if (pl.k1v && k == 19) return pl.c16 ? k_tile_pack<FMT, LP, 19, true, true, 1>
-                                                         : k_tile_pack<FMT, LP, 19, true, false, 1>;
-                } else if constexpr (S) {  // runtime-length layouts: plain counters only (make_plan)
-                    if (pl.k1v && k == 10) return k_tile_pack<FMT, LP, 10, true, false, 1>;
-                    if (pl.k1v && k == 19) return k_tile_pack<FMT, LP, 19, true, false, 1>;
-                }
-                return k == 10 ? (pl.c16 ? k_tile_pack<FMT, LP, 10, S, true> : k_tile_pack<FMT, LP, 10, S>)
-                     : k == 4  ? (pl.c16 ? k_tile_pack<FMT, LP, 4, S, true> : k_tile_pack<FMT, LP, 4, S>)
-                     : k == 19 ? (pl.c16 ? k_tile_pack<FMT, LP, 19, S, true> : k_tile_pack<FMT, LP, 19, S>)
-                     : k == 9  ? k_tile_pack<FMT, LP, 9, S>
-                               : k_tile_pack<FMT, LP, 0, false>;
-            };
-            auto fn = m <= (1u << 31) ? pick.template operator()<true>() : pick.template operator()<false>();
-            // the segment counters sit at LDS address 0: no static LDS may precede them
-            hipFuncAttributes fa{};
-            err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
-            if (err == hipSuccess && fa.sharedSizeBytes != 0) err = hipErrorInvalidKernelFile;
-            if (err == hipSuccess)
-                err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds1);
-            if (err == hipSuccess)
-                hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v == 1 ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles,
-                                   pl.ends_t ? endsT : ends, (uint16_t*)nullptr);
-        });
+        } else {
+            err = launch_tile_pack_main(pick_fmt(dk.keys, dk.offsets, dk.stride), kb.len_prefix, dk, pl, ntiles, tiles,
+                                        pl.ends_t ? endsT : ends, s);
+        }
         if (err != hipSuccess) return err;
         phase_end(kPhaseTileSort, s);
         if (!pl.ends_t) {

@@ -80,6 +80,21 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
 }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// The tile image is read back only by k_seg_or after this launch (2.5 GB at config 2: far beyond
+// the L2 and the Infinity Cache), so its copy-out is a streaming store (VBF_IMAGE_NT, default on):
+// it does not evict from the L2 the key bytes and offsets the other workgroups of the XCD are still
+// reading (config 3's keys are read in length order, every line several times).
+#ifndef VBF_IMAGE_NT
+#define VBF_IMAGE_NT 1
+#endif
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void image_store(uint32_t* dst, u32x4 v) {
+    if constexpr (VBF_IMAGE_NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+    else
+        *reinterpret_cast<u32x4*>(dst) = v;
+}
 __device__ __forceinline__ void lds_add(lds_u32* p) {
     (void)__hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -400,7 +415,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     const uint32_t words = group_words(total);
     for (uint32_t w = tid * 4; w < words; w += BS * 4) {
         if (w + 4 <= words)
-            *reinterpret_cast<uint4*>(out + w) = *reinterpret_cast<const uint4*>(smem + w);
+            image_store(out + w, *reinterpret_cast<const u32x4*>(smem + w));
         else
             for (uint32_t x = w; x < words; ++x) out[x] = smem[x];
     }
@@ -427,6 +442,17 @@ uint32_t group_pack_slots(uint32_t k);
 // the general m > 2^31 kernel).
 hipError_t launch_tile_pack_sat(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles,
                                 uint16_t* ends, hipStream_t s);
+// The compiled-k K1 of the build (vbf_tile_pack_main.hpp): launch_tile_pack_main dispatches the
+// key layout to launch_tile_pack_main_a (16/32-byte rows), _b (8/24) or _c (offsets, runtime
+// stride), each in a translation unit of its own.
+hipError_t launch_tile_pack_main(int fmt, bool lp, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                 uint32_t* tiles, uint16_t* ends, hipStream_t s);
+hipError_t launch_tile_pack_main_a(int fmt, bool lp, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                   uint32_t* tiles, uint16_t* ends, hipStream_t s);
+hipError_t launch_tile_pack_main_b(int fmt, bool lp, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                   uint32_t* tiles, uint16_t* ends, hipStream_t s);
+hipError_t launch_tile_pack_main_c(int fmt, bool lp, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                   uint32_t* tiles, uint16_t* ends, hipStream_t s);
 hipError_t launch_group_pack(const KeyBatch& kb, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                              uint32_t* tiles, uint16_t* endsT, uint16_t* posv, int sb, hipStream_t s);
 
