@@ -39,6 +39,9 @@ def make_parser():
     ap.add_argument("--keys", type=int, default=None)
     ap.add_argument("--key-bytes", type=int, default=16)
     ap.add_argument("--bits-per-key", type=int, default=10)
+    ap.add_argument("--raw-keys", action="store_true",
+                    help="configs 2/4: hash the keys without the length prefix (len_prefix = 0: pre-encoded "
+                         "integer keys such as bf.rs:307-424's usize keys)")
     ap.add_argument("--neg-keys", type=int, default=None)
     ap.add_argument("--e2e", action="store_true")
     ap.add_argument("--e2e-fresh-out", action="store_true", help="--e2e: a fresh host array per step")
@@ -357,12 +360,12 @@ def host_cpu_info():
             "usable_cores": usable}
 
 
-def cpu_baseline(keys_host, offsets_host, stride, n_sample, m, k, sample_desc, threads=1):
+def cpu_baseline(keys_host, offsets_host, stride, n_sample, m, k, sample_desc, threads=1, lp=1):
     """The oracle (a port of bf.rs:126-128 -> :84-92) on this node's host cores."""
     import oracle
     from velarixdb_amd.keys import HostBatch
     words = np.zeros((m + 31) // 32, np.uint32)
-    b = HostBatch(keys_host, offsets_host, stride, n_sample, 1)
+    b = HostBatch(keys_host, offsets_host, stride, n_sample, lp)
     t0 = time.perf_counter()
     oracle.build_words(b, m, k, words=words, threads=threads)
     dt = time.perf_counter() - t0
@@ -378,6 +381,7 @@ def bench_fixed(ctx, args):
     rank r builds SSTable shard r -- 50M keys, m = 5e8, seed 0x5EED0040 + r -- as one merged
     table's filter of a compaction (compactors/sized.rs:170-200, filter at :192-193)."""
     L = args.key_bytes
+    lp = 0 if args.raw_keys else 1
     w = rank_workload(args, ctx.rank)
     n, m, k, seed = w["keys"], w["m"], w["k"], w["seed"]
     keys = torch.empty(n * L, dtype=torch.uint8, device=ctx.dev)
@@ -393,7 +397,7 @@ def bench_fixed(ctx, args):
         if evs is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(ctx.stream)
-        call("vbf_build_dev_ex", vp(keys), None, L, n, 1, m, k, vp(words), build_strategy(args), ctx.sp)
+        call("vbf_build_dev_ex", vp(keys), None, L, n, lp, m, k, vp(words), build_strategy(args), ctx.sp)
         if evs is not None:
             b.record(ctx.stream)
             evs.append((a, b))
@@ -403,12 +407,12 @@ def bench_fixed(ctx, args):
 
     # post-timing checks on the last build: every key present; fill ratio
     cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
-    call("vbf_probe_count_dev", vp(keys), None, L, n, 1, m, k, vp(words), vp(cnt), ctx.sp)
+    call("vbf_probe_count_dev", vp(keys), None, L, n, lp, m, k, vp(words), vp(cnt), ctx.sp)
     pop = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
     call("vbf_popcount_dev", vp(words), nwords, vp(pop), ctx.sp)
     torch.cuda.synchronize()
     assert int(cnt.item()) == n, "false negatives: %d of %d keys found" % (cnt.item(), n)
-    sweep = time_probe_strategies(ctx, lambda st: call("vbf_probe_count_dev_ex", vp(keys), None, L, n, 1, m, k,
+    sweep = time_probe_strategies(ctx, lambda st: call("vbf_probe_count_dev_ex", vp(keys), None, L, n, lp, m, k,
                                                        vp(words), vp(cnt), st, ctx.sp))
 
     total_keys = ctx.sum_over_ranks(n) * args.steps
@@ -422,10 +426,11 @@ def bench_fixed(ctx, args):
     achieved = n * bytes_per_key / dom_s / 1e9
     # the contract's traffic: HBM bytes of one launch of the dominant kernel (like `achieved`);
     # the whole build's bytes beside it
-    dom_kernel = (ROCPROF.get((L, k), ({}, None))[0] or {}).get(dom)
+    rp = ROCPROF.get((L, k), (None, None)) if lp else (None, None)
+    dom_kernel = (rp[0] or {}).get(dom)
     traffic_file = {10: "traffic_config2.json", 19: "traffic_config2_k19.json"}.get(k)
     traffic, traffic_build, traffic_src = (pmc_traffic(traffic_file, dom_kernel)
-                                           if (n, L) == (100_000_000, 16) and traffic_file and args.strategy != 1
+                                           if (n, L, lp) == (100_000_000, 16, 1) and traffic_file and args.strategy != 1
                                            else (None, None, None))
     per_rank = ctx.gather({"rank": ctx.rank, "device": ctx.local, "keys": n, "seed": seed,
                            "keys_per_s": n * args.steps / rank_wall, "ms_per_step": rank_wall / args.steps * 1e3,
@@ -433,10 +438,11 @@ def bench_fixed(ctx, args):
     cfg_name = ("config4: %d independent SSTable shards x %dM x %dB keys, one per GPU (compaction fan-in), "
                 "%d bits/key (m=%d, k=%d per shard)" % (ctx.world, n // 10**6, L, args.bits_per_key, m, k)
                 if args.config == 4 else
-                "config2: %dM x %dB keys%s, %d bits/key (m=%d, k=%d)" % (
-                    n // 10**6, L, "" if ctx.world == 1 else " per GPU", args.bits_per_key, m, k))
+                "config2: %dM x %dB keys%s%s, %d bits/key (m=%d, k=%d)" % (
+                    n // 10**6, L, "" if ctx.world == 1 else " per GPU",
+                    " hashed without the length prefix" if not lp else "", args.bits_per_key, m, k))
     # the SQ pass of the same build shape (config 2's 100M x 16 B keys at k = 10 or 19)
-    sq = pmc_sq(SQ_FILES[k], 100_000_000) if (n, L) == (100_000_000, 16) and k in SQ_FILES else None
+    sq = pmc_sq(SQ_FILES[k], 100_000_000) if (n, L, lp) == (100_000_000, 16, 1) and k in SQ_FILES else None
     res = {
         "metric": "Bloom build keys/s (device-resident keys, bit-exact SipHash-1-3 filter)",
         "value": value, "unit": "keys/s", "n_gpus": ctx.world, "steps": args.steps,
@@ -444,14 +450,14 @@ def bench_fixed(ctx, args):
         "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
         "key_gib_per_s": value * L / 2**30,
         "config": {"workload": cfg_name, "baseline_config": args.config,
-                   "n_keys_per_gpu": n, "key_bytes": L, "m_bits": m, "k": k, "len_prefix": True,
+                   "n_keys_per_gpu": n, "key_bytes": L, "m_bits": m, "k": k, "len_prefix": bool(lp),
                    "parallelism": "independent shards x%d" % ctx.world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_build": traffic_build,
                      "traffic_source": traffic_src, "kernel": dom, "kernel_ms": dom_s * 1e3,
                      "build_ms": kavg * 1e3, "build_frac": n * bytes_per_key / kavg / 1e9 / HBM_PEAK_GBS,
-                     "rocprof_kernels": ROCPROF.get((L, k), (None, None))[0],
-                     "rocprof_summary": ROCPROF.get((L, k), (None, None))[1],
+                     "rocprof_kernels": rp[0],
+                     "rocprof_summary": rp[1],
                      "valu_frac_est": (n * sq["valu_lane_instr_per_key"] / dom_s / VALU_PEAK_LANE_OPS
                                        if sq else None),
                      "sq_counters": sq,
@@ -470,14 +476,14 @@ def bench_fixed(ctx, args):
         res["host_cpu"] = info
         res["cpu_baseline"] = cpu_baseline(host, None, L, ns, m, k,
                                            "first %d of the %d keys, same m=%d/k=%d, 1 thread, ref-faithful "
-                                           "(full SipHash per seed, u64 %%, serial like bf.rs:127)" % (ns, n, m, k))
+                                           "(full SipHash per seed, u64 %%, serial like bf.rs:127)" % (ns, n, m, k), lp=lp)
         t = args.cpu_opt_threads or info["usable_cores"]
         if t:
             res["cpu_opt"] = cpu_baseline(host, None, L, ns, m, k,
                                           "same sample, prefix-shared hashing, %d threads = every core this process "
                                           "may use (%s; %d logical CPUs on the machine)" % (
                                               t, info["model"] or "unknown CPU", info["logical_cpus"]),
-                                          threads=t)
+                                          threads=t, lp=lp)
     return res
 
 

@@ -562,6 +562,44 @@ def test_partitioned_build_knobs_same_words(vbf, ora, tmp_path):
                 assert np.array_equal(got, want[(m, k)]), (k1, et, k3, sp, m, k)
 
 
+@pytest.mark.parametrize("layout,m,k", [
+    ("usize", 14_377_000, 14),       # p = 1e-3 over usize keys (bf.rs:307-424's encoding): class 16
+    ("usize", 4_294_967_295, 6),     # saturated m, class 8 with the end-around-carry remainder
+    ("i32", 9_000_011, 7),           # 4-byte rows: the runtime-stride layout, class 8
+    ("vec_i32", 23_000_003, 23),     # &Vec<i32>: LE64(len) || LE32 x len, offsets layout, class 24
+    ("usize", 3_000_000_017, 31),    # m > 2^31 (Barrett), class 32
+])
+def test_runtime_k_classes_without_length_prefix(vbf, ora, layout, m, k):
+    """Missing r04 #4: batches hashed without the length prefix (len_prefix = 0: the pre-encoded
+    integer keys of bf.rs:275-424) at k outside {4, 9, 10, 19} take the runtime-k class kernels
+    (vbf_partition_rk_c.hip) instead of the scratch-stash kernel: words equal the oracle's."""
+    from velarixdb_amd.keys import HostBatch
+    rng = np.random.default_rng(k)
+    n = 400_000
+    if layout == "usize":
+        data = np.arange(n, dtype="<u8").view(np.uint8)
+        b = HostBatch(data, None, 8, n, 0)
+    elif layout == "i32":
+        data = rng.integers(-2**31, 2**31 - 1, n, dtype=np.int64).astype("<i4").view(np.uint8)
+        b = HostBatch(data, None, 4, n, 0)
+    else:
+        lens = rng.integers(0, 9, n)
+        parts, off = [], [0]
+        for j, c in enumerate(lens):
+            msg = np.uint64(c).tobytes() + rng.integers(-2**31, 2**31 - 1, int(c), dtype=np.int64).astype("<i4").tobytes()
+            parts.append(msg)
+            off.append(off[-1] + len(msg))
+        b = HostBatch(np.frombuffer(b"".join(parts), np.uint8).copy(), np.asarray(off, np.uint64), 0, n, 0)
+    got = gpu_build(vbf, b, m, k, strategy=PARTITIONED)
+    if m > 100_000_000:
+        nz = np.flatnonzero(got)
+        bits = np.unpackbits(got[nz].view(np.uint8), bitorder="little").reshape(-1, 32).astype(bool)
+        idx = np.sort((nz.astype(np.uint64)[:, None] * np.uint64(32) + np.arange(32, dtype=np.uint64))[bits])
+        assert np.array_equal(idx, np.unique((ora.hashes(b, k) % np.uint64(m)).ravel()))
+    else:
+        assert np.array_equal(got, ora.build_words(b, m, k, threads=8))
+
+
 # (m, k, layout) the kernel-selecting knobs gate: m = 2^32 - 1 (SAT / Barrett, k = 4 / 6 / 10 / 19,
 # fixed and runtime-length keys), the runtime-k classes (k = 7, 14, 23), k = 19 and 10 on the 512-
 # and 1 024-thread shapes; `probe`: the partitioned probe is also run (round-3 pipeline: VBF_Q3)

@@ -248,12 +248,12 @@ def test_config3_full_size_bit_exact(vbf, ora):
 
 
 def test_multi_chunk_partitioned_paths(vbf):
-    """More bit indices in one call than one chunk holds (build: kBuildChunkIdx = 2^31, probe:
+    """More bit indices in one call than one chunk holds (build: kBuildChunkIdx = 2^32, probe:
     kPartChunkIdx = 2^30): both partitioned paths process the batch in chunks.  The chunked
     build must equal the per-key atomic build bit for bit, and both probe strategies must find
     every key."""
     from velarixdb_amd.workloads import SEED_CFG2
-    n, L, m, k = 220_000_000, 16, 2_200_000_000, 10  # 2.2e9 indices: 2 build / 3 probe chunks
+    n, L, m, k = 440_000_000, 16, 4_000_000_000, 10  # 4.4e9 indices: 2 build / 5 probe chunks
     keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
     vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG2 ^ 0x77, 0, n, L, vp(keys), sp())
     w_part = build(vbf, keys, None, L, n, m, k, 2)

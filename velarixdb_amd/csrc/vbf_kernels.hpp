@@ -36,10 +36,12 @@ void phase_end(int phase, hipStream_t s);
 
 // Partitioned build (vbf_partition.hip).  Key batches are processed in chunks of at most
 // kBuildChunkIdx (build) / kPartChunkIdx (probe) bit indices; the workspace holds one chunk's
-// sorted tiles + offset tables (build: 2.5 B per index, ~5.4 GB at 2^31; probe: 4 B per index).
-// Each build chunk re-reads and re-writes the whole filter in k_seg_or, so build chunks are big.
+// sorted tiles + offset tables (build: 2.5 B per index, ~10.7 GB at 2^32; probe: 4 B per index).
+// Each build chunk re-reads and re-writes the whole filter in k_seg_or, so build chunks are big:
+// 2^32 holds config 5's 1B keys x k = 4 in one chunk (26.9 -> 26.5 ms: one k_seg_or pass over
+// the 512 MiB filter instead of two, and that one fresh; profiles/r05/ab_cfg5_single_chunk.txt).
 constexpr uint64_t kPartChunkIdx = 1ull << 30;
-constexpr uint64_t kBuildChunkIdx = 1ull << 31;
+constexpr uint64_t kBuildChunkIdx = 1ull << 32;
 bool partition_supported(uint32_t m, uint32_t k);
 uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
 // Partitioned probe (vbf_partition.hip): out (answer bytes) or count (hits), one of them.

@@ -480,7 +480,8 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     // any other k <= 32 (with the length prefix) takes a runtime-k class kernel on the 512-thread
     // shape, its stash in registers (VBF_KCLASS = 0: the generic scratch-stash kernel, A/B)
     static const int kcls = [] { const char* e = getenv("VBF_KCLASS"); return e ? atoi(e) : 1; }();
-    pl.kc = (!ck && kcls != 0 && lp) ? tile_pack_class(k) : 0u;
+    pl.kc = (!ck && kcls != 0) ? tile_pack_class(k) : 0u;
+    pl.lp = lp ? 1u : 0u;
     // K1 shape (k1_shape): the 512-thread one-lane-per-key workgroups where they exist (compiled
     // k = 10 / 19, a scan of <= 4 * 512 segments), by default (profiles/r03/matrix1.log, one box:
     // k = 19 tile_sort 6.76 -> 6.24 ms; k = 10 even with packed counters, and with plain ones
@@ -583,8 +584,18 @@ bool partition_supported(uint32_t m, uint32_t k) {
     return true;
 }
 
+// Bit indices per build chunk: kBuildChunkIdx, or 2^VBF_BUILD_CHUNK_LOG2 (speed only: each chunk's
+// k_seg_or re-reads and re-writes the whole filter, fewer chunks need a larger workspace)
+static uint64_t build_chunk_idx() {
+    static const uint64_t v = [] {
+        const char* e = getenv("VBF_BUILD_CHUNK_LOG2");
+        return e ? 1ull << std::max(20, std::min(33, atoi(e))) : kBuildChunkIdx;
+    }();
+    return v;
+}
+
 static uint64_t chunk_keys_for(const PartPlan& pl, uint64_t n) {
-    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, kBuildChunkIdx / pl.C);
+    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, build_chunk_idx() / pl.C);
     return std::min<uint64_t>(n, tiles_per_chunk * pl.KT);
 }
 
@@ -699,10 +710,12 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         pl.ntS = (ntiles + 7) & ~7u;
         hipError_t err = hipSuccess;
         phase_begin(kPhaseTileSort, s);
-        if (pl.kc) {  // a runtime-k class kernel (its own translation unit)
+        if (pl.kc) {  // a runtime-k class kernel (translation units of their own)
             const int fmt = pick_fmt(dk.keys, dk.offsets, dk.stride);
-            err = pl.kc <= 12 ? launch_tile_pack_class_a(fmt, dk, pl, ntiles, tiles, pl.ends_t ? endsT : ends, s)
-                              : launch_tile_pack_class_b(fmt, dk, pl, ntiles, tiles, pl.ends_t ? endsT : ends, s);
+            uint16_t* e = pl.ends_t ? endsT : ends;
+            err = !pl.lp        ? launch_tile_pack_class_c(fmt, dk, pl, ntiles, tiles, e, s)
+                  : pl.kc <= 12 ? launch_tile_pack_class_a(fmt, dk, pl, ntiles, tiles, e, s)
+                                : launch_tile_pack_class_b(fmt, dk, pl, ntiles, tiles, e, s);
         } else if (kb.len_prefix && m == 0xFFFFFFFFu &&
                    (err = launch_tile_pack_sat(pick_fmt(dk.keys, dk.offsets, dk.stride), dk, pl, ntiles, tiles,
                                                pl.ends_t ? endsT : ends, s)) != hipErrorNotSupported) {

@@ -4,6 +4,6 @@
 namespace vbf {
 hipError_t launch_tile_pack_class_b(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                                     uint32_t* tiles, uint16_t* ends, hipStream_t s) {
-    return launch_class_impl<16, 21, 24, 32>(fmt, dk, pl, ntiles, tiles, ends, s);
+    return launch_class_impl<true, 16, 21, 24, 32>(fmt, dk, pl, ntiles, tiles, ends, s);
 }
 }  // namespace vbf

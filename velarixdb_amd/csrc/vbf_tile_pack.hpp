@@ -29,6 +29,7 @@ struct PartPlan {
     uint32_t k1v;         // K1's workgroup shape (k1_shape; VBF_K1)
     uint32_t ends_t;      // K1 writes the run ends transposed, endsT[seg][tile] (VBF_ENDS_T)
     uint32_t kc;          // K1 runtime-k class: k <= kc seeds per key in a kc-slot stash (0: none)
+    uint32_t lp;          // the batch hashes the length prefix (selects the class kernels' LP)
     uint32_t gd_words;    // group pack: LDS words of its per-segment u16 table (0 for the build)
     uint32_t CPg;         // group pack: entries per tile in HBM, every run padded to whole groups
     uint32_t nfull;       // K3: segments [0, nfull) one workgroup each; the rest split in P parts
@@ -285,8 +286,11 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
             // half of its first SipRound (seed_hash, sip13.hpp)
             SeedCtx q{};
             if constexpr (FMT > 0) q = seed_ctx(p);
-#pragma unroll
-            for (int i = 0; i < KL; ++i) {
+            // one instance per seed slot with i a compile-time constant (a fold, like the rounds):
+            // a `#pragma unroll` loop was left rolled for the 32-slot class with runtime-length keys
+            // and the Barrett remainder, which put the stash in scratch memory (272 B per lane)
+            auto seed = [&](auto ic) {
+                constexpr int i = decltype(ic)::value;
                 uint32_t idx = kSentinel;
                 // class kernels: seeds past the runtime k (wave-uniform) leave sentinels
                 if (valid && (SPL == 1 || seed0 + i < (uint32_t)K) && (KC == 0 || (uint32_t)i < pl.k)) {
@@ -295,7 +299,10 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
                     seg_count<C16, SB>(cnt0, idx);
                 }
                 stash[r * KL + i] = idx;
-            }
+            };
+            [&]<int... Is>(std::integer_sequence<int, Is...>) {
+                (seed(std::integral_constant<int, Is>{}), ...);
+            }(std::make_integer_sequence<int, KL>{});
         };
         [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
             (round(std::integral_constant<int, Rs>{}), ...);

@@ -1,7 +1,8 @@
 // vbf_tile_pack_rk.hpp -- launch of the runtime-k class kernels of K1 (k_tile_pack<..., KC>), for
-// k outside the compiled set {4, 9, 10, 19}.  Included by the two class translation units
-// (vbf_partition_rk_a.hip: classes 5, 8, 12; vbf_partition_rk_b.hip: 16, 21, 24, 32), which the build
-// compiles in parallel with the rest of the library.
+// k outside the compiled set {4, 9, 10, 19}.  Included by the class translation units
+// (vbf_partition_rk_a.hip: classes 5, 8, 12; vbf_partition_rk_b.hip: 16, 21, 24, 32;
+// vbf_partition_rk_c.hip: every class for keys hashed without the length prefix -- the pre-encoded
+// integer keys of bf.rs:275-424), which the build compiles in parallel with the rest of the library.
 #pragma once
 #include <stdlib.h>
 
@@ -16,10 +17,13 @@ inline uint32_t tile_pack_class(uint32_t k) {
     return 0;
 }
 
-// Defined in vbf_partition_rk_a.hip (pl.kc <= 12) and vbf_partition_rk_b.hip (pl.kc >= 16).
+// Defined in vbf_partition_rk_a.hip (pl.kc <= 12), vbf_partition_rk_b.hip (pl.kc >= 16), both with
+// the length prefix, and vbf_partition_rk_c.hip (every class, no length prefix).
 hipError_t launch_tile_pack_class_a(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                                     uint32_t* tiles, uint16_t* ends, hipStream_t s);
 hipError_t launch_tile_pack_class_b(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                    uint32_t* tiles, uint16_t* ends, hipStream_t s);
+hipError_t launch_tile_pack_class_c(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                                     uint32_t* tiles, uint16_t* ends, hipStream_t s);
 
 // VBF_SAT=0 (A/B, speed only): Barrett remainders at m = 2^32 - 1 as well (vbf_partition_sat.hip)
@@ -30,13 +34,13 @@ inline bool sat_enabled() {
 
 // One class kernel: the segment counters sit at LDS address 0 (no static LDS may precede them),
 // the dynamic LDS request is the plan's.
-template <int FMT, int KC>
+template <int FMT, int KC, bool LP>
 hipError_t launch_one_class(const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles, uint16_t* ends,
                             hipStream_t s) {
     // m = 2^32 - 1 (the reference's saturated size): the end-around-carry remainder (SAT)
-    auto fn = pl.m <= (1ull << 31)        ? k_tile_pack<FMT, true, 0, true, false, 1, KC>
-              : pl.m == 0xFFFFFFFFull && sat_enabled() ? k_tile_pack<FMT, true, 0, false, false, 1, KC, kSegBits, false, true>
-                                                  : k_tile_pack<FMT, true, 0, false, false, 1, KC>;
+    auto fn = pl.m <= (1ull << 31)        ? k_tile_pack<FMT, LP, 0, true, false, 1, KC>
+              : pl.m == 0xFFFFFFFFull && sat_enabled() ? k_tile_pack<FMT, LP, 0, false, false, 1, KC, kSegBits, false, true>
+                                                  : k_tile_pack<FMT, LP, 0, false, false, 1, KC>;
     hipFuncAttributes fa{};
     hipError_t err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
     if (err == hipSuccess && fa.sharedSizeBytes != 0) err = hipErrorInvalidKernelFile;
@@ -48,19 +52,19 @@ hipError_t launch_one_class(const DevKeys& dk, const PartPlan& pl, uint32_t ntil
     return hipGetLastError();
 }
 
-template <int... KCs>
+template <bool LP, int... KCs>
 hipError_t launch_class_impl(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles,
                              uint16_t* ends, hipStream_t s) {
     hipError_t err = hipErrorInvalidValue;
     auto one = [&]<int KC>() {
         if (pl.kc != (uint32_t)KC) return;
         switch (fmt) {
-            case 16: err = launch_one_class<16, KC>(dk, pl, ntiles, tiles, ends, s); break;
-            case 32: err = launch_one_class<32, KC>(dk, pl, ntiles, tiles, ends, s); break;
-            case 8: err = launch_one_class<8, KC>(dk, pl, ntiles, tiles, ends, s); break;
-            case 24: err = launch_one_class<24, KC>(dk, pl, ntiles, tiles, ends, s); break;
-            case -1: err = launch_one_class<-1, KC>(dk, pl, ntiles, tiles, ends, s); break;
-            default: err = launch_one_class<0, KC>(dk, pl, ntiles, tiles, ends, s); break;
+            case 16: err = launch_one_class<16, KC, LP>(dk, pl, ntiles, tiles, ends, s); break;
+            case 32: err = launch_one_class<32, KC, LP>(dk, pl, ntiles, tiles, ends, s); break;
+            case 8: err = launch_one_class<8, KC, LP>(dk, pl, ntiles, tiles, ends, s); break;
+            case 24: err = launch_one_class<24, KC, LP>(dk, pl, ntiles, tiles, ends, s); break;
+            case -1: err = launch_one_class<-1, KC, LP>(dk, pl, ntiles, tiles, ends, s); break;
+            default: err = launch_one_class<0, KC, LP>(dk, pl, ntiles, tiles, ends, s); break;
         }
     };
     (one.template operator()<KCs>(), ...);
