@@ -713,9 +713,10 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         if (pl.kc) {  // a runtime-k class kernel (translation units of their own)
             const int fmt = pick_fmt(dk.keys, dk.offsets, dk.stride);
             uint16_t* e = pl.ends_t ? endsT : ends;
-            err = !pl.lp        ? launch_tile_pack_class_c(fmt, dk, pl, ntiles, tiles, e, s)
-                  : pl.kc <= 12 ? launch_tile_pack_class_a(fmt, dk, pl, ntiles, tiles, e, s)
-                                : launch_tile_pack_class_b(fmt, dk, pl, ntiles, tiles, e, s);
+            err = pl.kc <= 12 ? (pl.lp ? launch_tile_pack_class_a(fmt, dk, pl, ntiles, tiles, e, s)
+                                       : launch_tile_pack_class_c(fmt, dk, pl, ntiles, tiles, e, s))
+                              : (pl.lp ? launch_tile_pack_class_b(fmt, dk, pl, ntiles, tiles, e, s)
+                                       : launch_tile_pack_class_d(fmt, dk, pl, ntiles, tiles, e, s));
         } else if (kb.len_prefix && m == 0xFFFFFFFFu &&
                    (err = launch_tile_pack_sat(pick_fmt(dk.keys, dk.offsets, dk.stride), dk, pl, ntiles, tiles,
                                                pl.ends_t ? endsT : ends, s)) != hipErrorNotSupported) {

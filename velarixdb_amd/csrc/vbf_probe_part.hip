@@ -52,15 +52,19 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
             if (valid) p = key_prefix<FMT, LP>(dk, j);
             SeedCtx q{};
             if constexpr (FMT > 0) q = seed_ctx(p);  // block-aligned prefix: seed_hash (sip13.hpp)
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
+            // the seed slots as a fold with a compile-time slot number, as in k_tile_pack
+            auto seed = [&](auto ic) {
+                constexpr int i = decltype(ic)::value;
                 uint32_t idx = kSentinel;
                 if (valid) {
                     idx = mod_m<M31, SAT>(FMT > 0 ? seed_hash(q, i) : prefix_hash(p, i), pl.m, pl.mu);
                     atomicAdd(&cnt[idx >> SB], 1u);
                 }
                 stash[r * K + i] = idx;
-            }
+            };
+            [&]<int... Is>(std::integer_sequence<int, Is...>) {
+                (seed(std::integral_constant<int, Is>{}), ...);
+            }(std::make_integer_sequence<int, K>{});
         };
         [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
             (round(std::integral_constant<int, Rs>{}), ...);

@@ -1,8 +1,9 @@
 // vbf_tile_pack_rk.hpp -- launch of the runtime-k class kernels of K1 (k_tile_pack<..., KC>), for
 // k outside the compiled set {4, 9, 10, 19}.  Included by the class translation units
 // (vbf_partition_rk_a.hip: classes 5, 8, 12; vbf_partition_rk_b.hip: 16, 21, 24, 32;
-// vbf_partition_rk_c.hip: every class for keys hashed without the length prefix -- the pre-encoded
-// integer keys of bf.rs:275-424), which the build compiles in parallel with the rest of the library.
+// vbf_partition_rk_c.hip / _d.hip: the same classes for keys hashed without the length prefix -- the
+// pre-encoded integer keys of bf.rs:275-424), which the build compiles in parallel with the rest of
+// the library.
 #pragma once
 #include <stdlib.h>
 
@@ -17,13 +18,15 @@ inline uint32_t tile_pack_class(uint32_t k) {
     return 0;
 }
 
-// Defined in vbf_partition_rk_a.hip (pl.kc <= 12), vbf_partition_rk_b.hip (pl.kc >= 16), both with
-// the length prefix, and vbf_partition_rk_c.hip (every class, no length prefix).
+// Defined in vbf_partition_rk_a.hip (pl.kc <= 12) and vbf_partition_rk_b.hip (pl.kc >= 16), both with
+// the length prefix, and vbf_partition_rk_c.hip / _d.hip (the same, no length prefix).
 hipError_t launch_tile_pack_class_a(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                                     uint32_t* tiles, uint16_t* ends, hipStream_t s);
 hipError_t launch_tile_pack_class_b(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                                     uint32_t* tiles, uint16_t* ends, hipStream_t s);
 hipError_t launch_tile_pack_class_c(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                    uint32_t* tiles, uint16_t* ends, hipStream_t s);
+hipError_t launch_tile_pack_class_d(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                                     uint32_t* tiles, uint16_t* ends, hipStream_t s);
 
 // VBF_SAT=0 (A/B, speed only): Barrett remainders at m = 2^32 - 1 as well (vbf_partition_sat.hip)
