@@ -397,6 +397,12 @@ def test_async_set_failure_reported_by_next_call(vbf, ora):
          ctypes.cast(cb, ctypes.c_void_p), 8)
     with pytest.raises(VbfError):
         f.contains_batch(HostBatch(host[:L], None, L, 1, 1))
+    # the failed allocation's error stays with that job: the next set the device's worker thread
+    # runs, on another filter, succeeds (the sticky HIP error of the failed hipMalloc is cleared)
+    g = vbf.BloomFilter(0.01, n, device=f.device)
+    g.set_many_async(HostBatch(host, None, L, n, 1))
+    g.sync()
+    assert np.array_equal(g.words(), ora.build_words(HostBatch(host, None, L, n, 1), g.num_bits(), g.no_of_hash_func))
     assert f.contains_batch(HostBatch(host[:L], None, L, 1, 1)).all()
 
 

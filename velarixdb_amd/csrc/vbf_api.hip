@@ -48,10 +48,14 @@ inline int ok() {
     return VBF_OK;
 }
 
+// On failure the thread's sticky HIP error is cleared (hipGetLastError resets it) after it is
+// reported, so it cannot resurface as a later launch's hipGetLastError on the same thread -- e.g.
+// the next asynchronous set a device's worker thread runs after one whose allocation failed.
 #define HIP_TRY(expr)                                                                         \
     do {                                                                                      \
         hipError_t e_ = (expr);                                                               \
         if (e_ != hipSuccess) {                                                               \
+            (void)hipGetLastError();                                                          \
             int code_ = (e_ == hipErrorOutOfMemory) ? VBF_ENOMEM : VBF_EHIP;                  \
             return fail(code_, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
         }                                                                                     \
@@ -1047,6 +1051,7 @@ class AsyncQueue {
     static void run(AsyncJob& j) {
         Storage& s = *j.s;
         std::lock_guard<std::mutex> lk(s.mu);
+        (void)hipGetLastError();  // no earlier job's failure is this job's
         int rc;
         {
             DeviceGuard g(s.device);
@@ -1884,6 +1889,7 @@ int vbf_filter_migrate(vbf_filter* f, int device) {
         if (e == hipSuccess) e = zeros ? hipMemset(nd, 0, s.nwords * 4)
                                        : hipMemcpy(nd, w.data(), s.nwords * 4, hipMemcpyHostToDevice);
         if (e != hipSuccess) {  // the filter stays where it was, bits intact
+            (void)hipGetLastError();
             if (nd) (void)hipFree(nd);
             if (s.host()) s.h_words.swap(w);
             return fail(e == hipErrorOutOfMemory ? VBF_ENOMEM : VBF_EHIP, "moving the bits to device %d: %s",
