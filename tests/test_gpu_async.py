@@ -454,6 +454,69 @@ def test_fork_with_a_queued_set_fails_fast_in_the_child(vbf, ora):
     assert np.array_equal(fa.words(), _oracle_words(ora, 0x5EED0E40, n, fa.num_bits(), fa.no_of_hash_func))
 
 
+def _wait_child(pid, limit=60.0):
+    import os
+    import signal
+    import time
+    t0 = time.time()
+    while time.time() - t0 < limit:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            return status
+        time.sleep(0.05)
+    os.kill(pid, signal.SIGKILL)
+    os.waitpid(pid, 0)
+    raise AssertionError("the forked child hung")
+
+
+def test_forked_child_device_calls_fail_fast(vbf, ora):
+    """A child forked from a process that used the GPU through the library (nothing queued) gets
+    VBF_EINVAL ("forked") from every device-resident filter call instead of HIP calls that can
+    hang or fault: a synchronous build, a queued set (its worker reports the failure at the next
+    drain), single-key contains (the host mirror is the parent's pinned memory), a words copy and
+    a new device filter.  Host-resident filters keep working in the child.  The parent is unaffected."""
+    import os
+    from velarixdb_amd.filter import HOST
+    from velarixdb_amd.keys import HostBatch
+    n, L = 100_000, 16
+    h = ora.gen_fixed(0x5EED0E60, 0, n, L)
+    f = vbf.BloomFilter(0.01, n)
+    f.set_batch(HostBatch(h, None, L, n, 1))
+    assert f.contains(bytes(h[:L]))
+    pid = os.fork()
+    if pid == 0:
+        code = 10
+        try:
+            code = 0
+            probes = [
+                lambda: f.set_batch(HostBatch(h[:L * 10], None, L, 10, 1)),
+                lambda: (f.set_many_async(HostBatch(h[:L * 10], None, L, 10, 1)), f.sync()),
+                lambda: f.contains(bytes(h[:L])),
+                lambda: f.words(),
+                lambda: vbf.BloomFilter(0.01, 1000, device=f.device),
+            ]
+            for i, p in enumerate(probes):
+                try:
+                    p()
+                    code = 20 + i
+                    break
+                except AssertionError as e:
+                    if "forked" not in str(e):
+                        code = 40 + i
+                        break
+            if code == 0:  # the host path needs no GPU
+                g = vbf.BloomFilter(0.01, 1000, device=HOST)
+                g.set_batch(HostBatch(h[:L * 10], None, L, 10, 1))
+                if not g.contains(bytes(h[:L])):
+                    code = 60
+        finally:
+            os._exit(code)
+    status = _wait_child(pid)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, (status, os.WEXITSTATUS(status))
+    f.set_batch(HostBatch(h[:L * 10], None, L, 10, 1))
+    assert np.array_equal(f.words(), _oracle_words(ora, 0x5EED0E60, n, f.num_bits(), f.no_of_hash_func))
+
+
 def test_words_dev_read_keeps_the_mirror(vbf, ora):
     """the read-only pointer (vbf_filter_words_dev_read, the OR source of a
     merge) does not mark the filter externally written, so single-key contains keep answering

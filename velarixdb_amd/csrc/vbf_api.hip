@@ -62,14 +62,33 @@ inline int ok() {
     } while (0)
 
 // Switches the calling thread to `device` for the scope, restoring the previous one.
+// HIP does not survive fork(): a child of a process that used the GPU through this library must not
+// call into HIP (such calls can hang or fault).  The first device scope records the process that
+// uses HIP; a forked child's device scopes fail with VBF_EINVAL before any HIP call.
+std::atomic<pid_t> g_hip_pid{0};
+
+bool hip_forked() {
+    const pid_t owner = g_hip_pid.load();
+    return owner != 0 && owner != getpid();
+}
+
 struct DeviceGuard {
     int prev = -1;
     hipError_t err = hipSuccess;
+    bool forked = false;
     explicit DeviceGuard(int device) {
+        const pid_t me = getpid();
+        pid_t owner = 0;
+        if (!g_hip_pid.compare_exchange_strong(owner, me) && owner != me) {
+            forked = true;
+            err = hipErrorNotSupported;
+            return;
+        }
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
         if (prev != device) err = hipSetDevice(device);
     }
     ~DeviceGuard() {
+        if (forked) return;
         int cur = -1;
         if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
     }
@@ -77,6 +96,9 @@ struct DeviceGuard {
 
 #define DEVICE_SCOPE(dev)                                                                     \
     DeviceGuard guard_(dev);                                                                  \
+    if (guard_.forked)                                                                        \
+        return fail(VBF_EINVAL, "process %d forked from %d, which uses the GPU: HIP cannot be used " \
+                    "in the child", (int)getpid(), (int)g_hip_pid.load());                    \
     if (guard_.err != hipSuccess)                                                             \
         return fail(VBF_ENODEV, "hipSetDevice(%d): %s", (int)(dev), hipGetErrorString(guard_.err))
 
@@ -598,11 +620,15 @@ struct Storage {
     bool mirror_current() const { return mirror_ok && !ext_write; }
     bool host() const { return device == VBF_DEVICE_HOST; }
     void free_mirror() {
-        if (mirror) (void)hipHostFree(mirror);
+        if (mirror && !hip_forked()) (void)hipHostFree(mirror);
         mirror = nullptr;
         mirror_ok = false;
     }
     ~Storage() {
+        if (hip_forked()) {  // a forked child: the allocations are the parent's, and HIP is off limits
+            mirror = nullptr;
+            return;
+        }
         if (d_words) {
             int prev = -1;
             (void)hipGetDevice(&prev);
@@ -1051,12 +1077,18 @@ class AsyncQueue {
     static void run(AsyncJob& j) {
         Storage& s = *j.s;
         std::lock_guard<std::mutex> lk(s.mu);
-        (void)hipGetLastError();  // no earlier job's failure is this job's
         int rc;
         {
             DeviceGuard g(s.device);
-            rc = g.err != hipSuccess ? fail(VBF_ENODEV, "hipSetDevice(%d): %s", s.device, hipGetErrorString(g.err))
-                                     : device_set_host(s, j.k, j.keys, j.offsets, j.stride, j.n, j.lp);
+            if (g.forked) {
+                rc = fail(VBF_EINVAL, "process %d forked from %d, which uses the GPU: HIP cannot be used in the child",
+                          (int)getpid(), (int)g_hip_pid.load());
+            } else if (g.err != hipSuccess) {
+                rc = fail(VBF_ENODEV, "hipSetDevice(%d): %s", s.device, hipGetErrorString(g.err));
+            } else {
+                (void)hipGetLastError();  // no earlier job's failure is this job's
+                rc = device_set_host(s, j.k, j.keys, j.offsets, j.stride, j.n, j.lp);
+            }
         }
         if (rc && s.async_rc == VBF_OK) {  // the first failure is reported by the next call that drains
             s.async_rc = rc;
