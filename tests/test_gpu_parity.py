@@ -608,13 +608,14 @@ KNOB_CASES = (
     (4_294_967_295, 10, "f16", False), (4_294_967_295, 19, "f16", True), (4_294_967_295, 4, "var", True),
     (4_294_967_295, 7, "var", False), (20_000_003, 7, "f16", True), (30_000_001, 14, "var", False),
     (40_000_000, 23, "f32", False), (3_800_017, 19, "f16", False), (10_000_000, 10, "var", False),
-    (6_000_011, 10, "f16", True),
+    (6_000_011, 10, "f16", True), (200_000_003, 19, "f16", True), (300_000_001, 10, "var", True),
+    (150_000_007, 10, "f32", False), (100_000_007, 19, "var", False),
 )
 # every kernel-changing knob of DESIGN.md section 8b that VERDICT r04 found untested (one child each;
 # the library reads them once per process)
 KNOB_COMBOS = (
     {"VBF_SAT": "0"}, {"VBF_KCLASS": "0"}, {"VBF_K1_4": "1"}, {"VBF_C16": "0"}, {"VBF_C16": "1"},
-    {"VBF_C16": "1", "VBF_K1": "0"}, {"VBF_Q3": "0"}, {},
+    {"VBF_C16": "1", "VBF_K1": "0"}, {"VBF_Q3": "0"}, {}, {"VBF_K1W": "1"}, {"VBF_K1W": "2"}, {"VBF_K1W": "3"},
 )
 
 
@@ -624,7 +625,10 @@ def test_kernel_knobs_same_words(vbf, ora, tmp_path):
     (k = 4 on the 512-thread shape: the case whose packed-counter scan was once wrong),
     VBF_C16=0/1 (plain or packed segment counters, on either K1 shape), VBF_Q3=0 (the partitioned
     probe's one-pass segment test) -- give the oracle's words (bf.rs:84-92) and probe answers
-    (bf.rs:95-105) at the shapes they gate.  Each setting runs in a child process; the parent
+    (bf.rs:95-105) at the shapes they gate.  Round 5: VBF_K1W=1/2/3 (the two-window K1, its
+    balanced-window and direct-placement test modes); the builds are explicitly partitioned
+    (VBF_BUILD_PARTITIONED: at 300K keys AUTO would take the atomic kernel for k <= 13, so the K1
+    knobs were not exercised there before).  Each setting runs in a child process; the parent
     compares every child's words and answers with the oracle's."""
     import subprocess
     import sys
@@ -660,9 +664,13 @@ def test_kernel_knobs_same_words(vbf, ora, tmp_path):
         "res = {}\n"
         "for i, (m, k, lay, probe) in enumerate(%r):\n"
         "    b = B[lay]\n"
-        "    w = np.zeros((m + 31) // 32, np.uint32)\n"
-        "    d, o = b.ptrs()\n"
-        "    v._lib.call('vbf_build_host', d, o, b.stride, b.n, 1, m, k, w.ctypes.data, w.size, 0)\n"
+        "    kd0 = torch.from_numpy(b.data).cuda()\n"
+        "    od0 = torch.from_numpy(b.offsets.view(np.int64)).cuda() if b.offsets is not None else None\n"
+        "    wd0 = torch.zeros((m + 31) // 32, dtype=torch.int32, device='cuda')\n"
+        "    v._lib.call('vbf_build_dev_ex', vp(kd0), vp(od0), b.stride, b.n, 1, m, k, vp(wd0), 2, None)\n"
+        "    torch.cuda.synchronize()\n"
+        "    w = wd0.cpu().numpy().view(np.uint32)\n"
+        "    del kd0, od0, wd0\n"
         "    nz = np.flatnonzero(w)\n"
         "    res['nz%%d' %% i], res['w%%d' %% i] = nz.astype(np.uint64), w[nz]\n"
         "    if probe:\n"
