@@ -615,7 +615,7 @@ KNOB_CASES = (
 # the library reads them once per process)
 KNOB_COMBOS = (
     {"VBF_SAT": "0"}, {"VBF_KCLASS": "0"}, {"VBF_K1_4": "1"}, {"VBF_C16": "0"}, {"VBF_C16": "1"},
-    {"VBF_C16": "1", "VBF_K1": "0"}, {"VBF_Q3": "0"}, {}, {"VBF_K1W": "1"}, {"VBF_K1W": "2"}, {"VBF_K1W": "3"},
+    {"VBF_C16": "1", "VBF_K1": "0"}, {"VBF_Q3": "0"}, {},
 )
 
 
@@ -625,10 +625,10 @@ def test_kernel_knobs_same_words(vbf, ora, tmp_path):
     (k = 4 on the 512-thread shape: the case whose packed-counter scan was once wrong),
     VBF_C16=0/1 (plain or packed segment counters, on either K1 shape), VBF_Q3=0 (the partitioned
     probe's one-pass segment test) -- give the oracle's words (bf.rs:84-92) and probe answers
-    (bf.rs:95-105) at the shapes they gate.  Round 5: VBF_K1W=1/2/3 (the two-window K1, its
-    balanced-window and direct-placement test modes); the builds are explicitly partitioned
+    (bf.rs:95-105) at the shapes they gate.  Round 5: the builds are explicitly partitioned
     (VBF_BUILD_PARTITIONED: at 300K keys AUTO would take the atomic kernel for k <= 13, so the K1
-    knobs were not exercised there before).  Each setting runs in a child process; the parent
+    knobs were not exercised at those shapes before), and four shapes of the 512-thread K1 with
+    m well above one segment were added.  Each setting runs in a child process; the parent
     compares every child's words and answers with the oracle's."""
     import subprocess
     import sys

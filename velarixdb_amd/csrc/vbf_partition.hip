@@ -512,6 +512,9 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     static const int k14env = [] { const char* e = getenv("VBF_K1_4"); return e ? atoi(e) : 0; }();
     static const int satenv = [] { const char* e = getenv("VBF_SAT"); return e ? atoi(e) : 1; }();
     if (k14env == 1 && satenv != 0 && k == 4 && fixed && lp && m == 0xFFFFFFFFu && !group && pl.c16) pl.k1v = 1;
+    const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : k), fixed, (int)pl.k1v);
+    const uint32_t rmax = (uint32_t)(ck || pl.kc ? sh.rounds : rounds_max((int)k));
+    const uint32_t kpr = (uint32_t)sh.bs / (uint32_t)(ck ? sh.spl : 1);  // keys per round
     // K1 writes endsT[seg][tile] itself, no transpose pass (k = 19: -0.15 ms per 100M keys, k = 10
     // -0.025 ms; VBF_ENDS_T = 0 keeps the transpose)
     static const int etenv = [] { const char* e = getenv("VBF_ENDS_T"); return e ? atoi(e) : 1; }();
@@ -519,33 +522,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     const uint32_t cnt_words = pl.c16 ? ((pl.nseg + 7) & ~7u) / 2 : pl.nseg_pad;
     pl.cnt_words = cnt_words;
     pl.gd_words = group ? (((pl.nseg + 1) / 2 + 3) & ~3u) : 0u;  // the group pack's u16 run table
-    // V = 2 (VBF_K1W = 1): the 512-thread shape with a larger stash and two placement windows
-    // (k_tile_pack / tile_pack_windows): longer runs for k_seg_or, one more pass over the stash in K1.
-    // Tests only: VBF_K1W = 2 shrinks the window to about half a tile (both windows always used),
-    // 3 to 4 096 entries (full tiles take the direct-to-HBM placement).
-    static const int k1wenv = [] { const char* e = getenv("VBF_K1W"); return e ? atoi(e) : 0; }();
-    if (k1wenv >= 1 && pl.k1v == 1 && !group && !pl.kc && !pl.c16 && pl.ends_t && m <= (1u << 31) &&
-        (k == 10 || k == 19)) {
-        const K1Shape sw = k1_shape((int)k, fixed, 2);
-        const int64_t avail = (int64_t)kLdsPerCu / 2 - 4 * (16 + kLenBuckets) - 4 * (int64_t)cnt_words - 4 * 16;
-        uint32_t capw = (uint32_t)std::max<int64_t>(0, avail / 4 / 5 * 8);  // 5 words per 8 entries
-        const uint32_t T = (uint32_t)sw.rounds * 512u * k;
-        // the split needs a segment boundary between T - capw and capw entries: with random keys
-        // there is one when a segment's run is well below that interval (nseg >= 4 T / (2 capw - T))
-        const bool fits = T <= 65535 && T + 1024 <= 2 * capw && (uint64_t)pl.nseg * (2 * capw - T) >= 4ull * T;
-        if (k1wenv == 2) capw = std::min(capw, (T / 2 + 512) & ~7u);
-        if (k1wenv == 3) capw = std::min(capw, 4096u);
-        if (T <= 65535 && (fits || k1wenv >= 2)) {
-            pl.k1v = 2;
-            pl.capw = capw;
-        }
-    }
-    const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : k), fixed, (int)pl.k1v);
-    const uint32_t rmax = (uint32_t)(ck || pl.kc ? sh.rounds : rounds_max((int)k));
-    const uint32_t kpr = (uint32_t)sh.bs / (uint32_t)(ck ? sh.spl : 1);  // keys per round
-    if (pl.k1v == 2) {
-        pl.KT = rmax * kpr;
-    } else for (uint32_t per_cu : {2u, 1u}) {
+    for (uint32_t per_cu : {2u, 1u}) {
         const uint32_t budget = kLdsPerCu / per_cu;
         const int64_t avail = (int64_t)budget - 4 * (16 + kLenBuckets) - 4 * (int64_t)cnt_words - 4 * (int64_t)pl.gd_words;
         // LDS = 2.5 * CP with CP <= C + 7 (the group pack: runs padded to whole groups in LDS,
@@ -570,9 +547,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     static const int tpad = [] { const char* e = getenv("VBF_TILE_PAD"); return e ? atoi(e) : 4; }();
     pl.tile_words += (uint32_t)std::max(0, tpad) & ~3u;
     pl.nsegS = (pl.nseg + 7) & ~7u;
-    // the LDS image: the whole tile, or (V = 2) one window of capw entries + the moved boundary group
-    const uint32_t img_words = pl.k1v == 2 ? pl.capw / 8 * kGroupWords + 16 : group_words(group ? pl.CPg : pl.CP);
-    pl.lds1 = (img_words + cnt_words + 16 + kLenBuckets + pl.gd_words) * 4;
+    pl.lds1 = (group_words(group ? pl.CPg : pl.CP) + cnt_words + 16 + kLenBuckets + pl.gd_words) * 4;
     // VBF_TILE_LDS_MIN (experiments, speed only): request at least this much LDS per k_tile_pack
     // workgroup, e.g. > 80 KiB to hold one workgroup per CU
     static const int lds_min = [] { const char* e = getenv("VBF_TILE_LDS_MIN"); return e ? atoi(e) : 0; }();
@@ -595,7 +570,7 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     pl.len_order = (uint32_t)(lord != 0 && !group);  // the group pack's positions are in key order
     static const int stg = [] { const char* e = getenv("VBF_STAGE_KEYS"); return e ? atoi(e) : 1; }();
     // words: perm (KT u16) + begin + length (KT u32 each) inside the image's words
-    pl.stage_keys = (uint32_t)(stg != 0 && (uint64_t)(pl.KT + 1) / 2 + 2ull * pl.KT <= img_words);
+    pl.stage_keys = (uint32_t)(stg != 0 && (uint64_t)(pl.KT + 1) / 2 + 2ull * pl.KT <= group_words(pl.CP));
     return pl;
 }
 

@@ -59,19 +59,11 @@ __host__ __device__ constexpr int build_rounds_max(int k, bool fixed) {
 // kStashWide indices: k = 19 takes three rounds of 512 keys on one lane each (no idle 20th seed
 // slot, the prefix absorbed once), the same 1 536-key tile as V = 0.
 constexpr int kStashWide = 64;
-// V = 2 (the 512-thread shape with two placement windows, k = 10 / 19, m <= 2^31): a larger stash
-// (k = 19: four rounds, a 2 048-key tile; k = 10: eight, 4 096 keys) -- the LDS image holds about
-// half of such a tile, so k_tile_pack places and copies it out in two windows of segments.
-#ifndef VBF_STASH_W2
-#define VBF_STASH_W2 80
-#endif
-constexpr int kStashW2 = VBF_STASH_W2;
 struct K1Shape {
     int bs, spl, kl, rounds;
 };
 __host__ __device__ constexpr K1Shape k1_shape(int k, bool fixed, int v) {
     // k = 4 on this shape (m = 2^32 - 1, VBF_K1_4): fourteen rounds, a 7 168-key tile
-    if (v == 2) return K1Shape{512, 1, k, kStashW2 / k};
     if (v == 1) return K1Shape{512, 1, k, k == 4 ? 14 : kStashWide / k < 6 ? kStashWide / k : 6};
     return K1Shape{kPBlock, build_spl(k, fixed), build_kl(k, fixed), build_rounds_max(k, fixed)};
 }

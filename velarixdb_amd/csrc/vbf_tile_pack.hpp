@@ -34,7 +34,6 @@ struct PartPlan {
     uint32_t CPg;         // group pack: entries per tile in HBM, every run padded to whole groups
     uint32_t nfull;       // K3: segments [0, nfull) one workgroup each; the rest split in P parts
     uint32_t P;
-    uint32_t capw;        // K1 shape V = 2: entries one placement window of the LDS image holds
     uint64_t m, mu, nwords;
 };
 
@@ -82,11 +81,6 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
 }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-
-// V = 2 kernels hash their rounds in a rolled loop (k_tile_pack); 0 unrolls them as V = 1 does (A/B)
-#ifndef VBF_W2_FIFO
-#define VBF_W2_FIFO 1
-#endif
 
 // The tile image is read back only by k_seg_or after this launch (2.5 GB at config 2: far beyond
 // the L2 and the Infinity Cache), so its copy-out is a streaming store (VBF_IMAGE_NT, default on):
@@ -149,118 +143,6 @@ __device__ __forceinline__ uint32_t seg_get(const uint32_t* cnt, uint32_t s) {
 constexpr uint32_t kGroupWords = 5;
 __host__ __device__ constexpr uint32_t group_words(uint32_t entries) { return (entries + 7) / 8 * kGroupWords; }
 
-// Rank + place of the stash entries whose segment lies in [s_lo, s_hi) into an LDS image whose
-// group 0 is the tile's group g0, starting at LDS word d (d == 5 * g0 mod 4, so LDS and HBM words
-// of the image agree mod 4), 8 returning LDS atomics in flight before their results are used.
-template <int SB, int NS>
-__device__ __forceinline__ void place_window(const uint32_t (&stash)[NS], uint32_t ns, lds_u32* cnt0, uint32_t* smem,
-                                             uint16_t* lo, uint32_t s_lo, uint32_t s_hi, uint32_t g0, uint32_t d) {
-#pragma unroll
-    for (uint32_t t = 0; t < (uint32_t)NS; t += 8) {
-        if (t >= ns) break;
-        uint32_t pos[8], val[8];
-        bool in[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            val[q] = (t + q < (uint32_t)NS && t + q < ns) ? stash[t + q] : kSentinel;
-            const uint32_t sg = val[q] >> SB;
-            in[q] = val[q] != kSentinel && sg >= s_lo && sg < s_hi;
-            pos[q] = in[q] ? seg_rank<false, SB>(cnt0, val[q]) : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (in[q]) {
-                const uint32_t g = d + ((pos[q] >> 3) - g0) * kGroupWords, e7 = pos[q] & 7;
-                lo[g * 2 + e7] = (uint16_t)val[q];
-                atomicOr(&smem[g + 4], ((val[q] >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4));
-            }
-        }
-    }
-}
-
-// HBM words [h0, h1) of a tile image from LDS words [l0, ..) (l0 == h0 mod 4, l0 >= h0 mod 4):
-// whole 16-byte chunks inside the range as streaming vector stores, the words of a chunk that the
-// range cuts one by one (the neighbouring words belong to the other window).
-template <int BS>
-__device__ __forceinline__ void copy_window(uint32_t* out, const uint32_t* smem, uint32_t h0, uint32_t h1, uint32_t l0) {
-    for (uint32_t a = (h0 & ~3u) + threadIdx.x * 4; a < h1; a += BS * 4) {
-        const uint32_t l = a - h0 + l0;
-        if (a >= h0 && a + 4 <= h1) {
-            image_store(out + a, *reinterpret_cast<const u32x4*>(smem + l));
-        } else {
-            for (uint32_t x = a < h0 ? h0 : a; x < a + 4 && x < h1; ++x) out[x] = smem[x - h0 + l0];
-        }
-    }
-}
-
-// K1 shape V = 2: the tile holds more entries (T) than the LDS image (pl.capw per window), so the
-// segments are placed in two windows -- [0, s1) with s1 the last segment boundary at or below
-// capw entries, then [s1, nseg) -- each copied out before the next; the group that the window
-// boundary cuts moves to the front of the second window's image.  The stash stays in registers
-// across both.  Ranks come from the same per-segment counters, so after both windows cnt[s] is
-// the end of segment s's run exactly as with one window.  When the second window would not fit
-// either (a segment of more than ~T - capw entries: heavily repeated keys), every entry goes
-// straight to its place in the HBM image (global stores and nibble atomics) instead.
-// Caller: the counters hold the exclusive starts and a barrier has passed; ends with the image in
-// HBM (a barrier is still needed before cnt[] is read as the run ends).
-template <int BS, int SB, int NS>
-__device__ __forceinline__ void tile_pack_windows(const PartPlan& pl, uint32_t (&stash)[NS], uint32_t ns, uint32_t T,
-                                                  uint32_t* cnt, lds_u32* cnt0, uint32_t* wsum, uint32_t* smem,
-                                                  uint16_t* lo, uint32_t* out) {
-    const uint32_t tid = threadIdx.x;
-    const uint32_t capw = pl.capw, nseg = pl.nseg, ng = (T + 7) >> 3;
-    if (tid == 0) wsum[0] = 0;
-    __syncthreads();
-    for (uint32_t sg = tid + 1; sg <= nseg; sg += BS)
-        if ((sg < nseg ? cnt[sg] : T) <= capw) atomicMax(&wsum[0], sg);
-    __syncthreads();
-    const uint32_t s1 = wsum[0];
-    const uint32_t P1 = s1 < nseg ? cnt[s1] : T;
-    if (T - P1 > capw) {
-        uint16_t* o16 = reinterpret_cast<uint16_t*>(out);
-        for (uint32_t g = tid; g < ng; g += BS) out[g * kGroupWords + 4] = 0;
-        __threadfence();
-        __syncthreads();
-        // one entry per iteration from stash[0], the stash shifted down after it: a rolled loop
-        // (this path is rare) whose stash indices are all static, so the stash stays in registers
-#pragma unroll 1
-        for (uint32_t t = 0; t < ns; ++t) {
-            const uint32_t v = stash[0];
-            if (v != kSentinel) {
-                const uint32_t pos = seg_rank<false, SB>(cnt0, v), g = (pos >> 3) * kGroupWords, e7 = pos & 7;
-                o16[g * 2 + e7] = (uint16_t)v;
-                atomicOr(&out[g + 4], ((v >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4));
-            }
-#pragma unroll
-            for (int i = 0; i + 1 < NS; ++i) stash[i] = stash[i + 1];
-        }
-        return;
-    }
-    const uint32_t G1 = P1 >> 3;  // the group the window boundary falls in
-    const uint32_t d = (G1 * kGroupWords) & 3u;
-    for (uint32_t g = tid; g <= G1 && g < ng; g += BS) smem[g * kGroupWords + 4] = 0;
-    __syncthreads();
-    // the two windows share one instance of the placement code (a rolled loop)
-#pragma unroll 1
-    for (uint32_t w = 0; w < 2; ++w) {
-        place_window<SB>(stash, ns, cnt0, smem, lo, w ? s1 : 0u, w ? nseg : s1, w ? G1 : 0u, w ? d : 0u);
-        __syncthreads();
-        if (w == 0 && s1 >= nseg) {  // one window held the tile
-            copy_window<BS>(out, smem, 0u, ng * kGroupWords, 0u);
-            break;
-        }
-        copy_window<BS>(out, smem, w ? G1 * kGroupWords : 0u, w ? ng * kGroupWords : G1 * kGroupWords, w ? d : 0u);
-        if (w == 0) {
-            uint32_t bw = 0;
-            if (tid < kGroupWords) bw = smem[G1 * kGroupWords + tid];
-            __syncthreads();
-            if (tid < kGroupWords) smem[d + tid] = bw;
-            for (uint32_t g = G1 + 1 + tid; g < ng; g += BS) smem[d + (g - G1) * kGroupWords + 4] = 0;
-            __syncthreads();
-        }
-    }
-}
-
 // K > 0: k known at compile time (the stash and seed loops unroll, no indexed register moves);
 // K == 0, KC > 0: a runtime-k class -- any k <= KC (pl.k) in the compiled kernel's KC-slot stash
 // (the seed loop unrolls to KC with a wave-uniform `i < k` guard, the unused slots hold sentinels),
@@ -277,12 +159,11 @@ __device__ __forceinline__ void tile_pack_windows(const PartPlan& pl, uint32_t (
 // SAT: m == 2^32 - 1 (the reference's saturated size), remainders by mod_sat (sip13.hpp).
 template <int FMT, bool LP, int K, bool M31, bool C16 = false, int V = 0, int KC = 0, int SB = kSegBits,
           bool POS = false, bool SAT = false>
-__global__ __launch_bounds__(V >= 1 ? 512 : kPBlock, V >= 1 ? 4 : 8) void k_tile_pack(DevKeys dk, PartPlan pl,
+__global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile_pack(DevKeys dk, PartPlan pl,
                                                                                       uint32_t* tiles, uint16_t* ends,
                                                                                       uint16_t* posv) {
-    constexpr int BS = V >= 1 ? 512 : kPBlock;  // k1_shape(K, FMT > 0, V).bs
+    constexpr int BS = V == 1 ? 512 : kPBlock;  // k1_shape(K, FMT > 0, V).bs
     static_assert(V == 0 || K > 0 || KC > 0, "the 512-thread shape is for compiled k and k classes");
-    static_assert(V != 2 || (K > 0 && M31 && !C16 && !POS && !SAT), "two windows: compiled k, m <= 2^31, plain counters");
     static_assert(KC == 0 || (K == 0 && V == 1 && !C16), "k classes run on the 512-thread shape");
     constexpr int KK = K > 0 ? K : KC;  // seed slots per key in the stash (0: the scratch stash)
     extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
@@ -358,7 +239,7 @@ __global__ __launch_bounds__(V >= 1 ? 512 : kPBlock, V >= 1 ? 4 : 8) void k_tile
         // Runtime-length layouts on the 512-thread shape (128 VGPRs): the first five source words
         // of a lane's next-round key are loaded before this round's absorb, so they arrive while
         // this round hashes (config 3: the absorb waited on its first loads).
-        constexpr bool PF = FMT <= 0 && V >= 1;
+        constexpr bool PF = FMT <= 0 && V == 1;
         auto key_span = [&](uint32_t slot, uint64_t& beg, uint64_t& len) {
             if constexpr (FMT < 0) {
                 if (staged) {
@@ -382,17 +263,15 @@ __global__ __launch_bounds__(V >= 1 ? 512 : kPBlock, V >= 1 ? 4 : 8) void k_tile
         };
         KeyHead head_cur{};
         if constexpr (PF) head_cur = head_of(0);
-        // V = 2's rolled round (the unrolled `round` below is the same work with a compile-time r;
-        // kept separate so the V = 0 / 1 kernels' code stays exactly as measured): r, whether a
-        // later round follows (the prefetch), and where seed slot i's index goes
-        auto round_body = [&](uint32_t r, bool next, auto&& store) {
-            const uint32_t slot = r * kKeysPerRound + tid / SPL;
+        auto round = [&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            const uint32_t slot = (uint32_t)r * kKeysPerRound + tid / SPL;
             const uint32_t seed0 = (uint32_t)KL * (tid % SPL);
-            const bool valid = r < pl.R && slot < nk;
+            const bool valid = (uint32_t)r < pl.R && slot < nk;
             Prefix p{};
             if constexpr (PF) {
                 const KeyHead h = head_cur;
-                if (next) head_cur = head_of(r + 1);
+                if constexpr (r + 1 < RM) head_cur = head_of(r + 1);
                 if (valid) p = key_prefix_head<LP>(h);
             } else if (valid) {
                 if constexpr (FMT < 0) {
@@ -419,66 +298,15 @@ __global__ __launch_bounds__(V >= 1 ? 512 : kPBlock, V >= 1 ? 4 : 8) void k_tile
                     idx = mod_m<M31, SAT>(h, pl.m, pl.mu);
                     seg_count<C16, SB>(cnt0, idx);
                 }
-                store(ic, idx);
+                stash[r * KL + i] = idx;
             };
             [&]<int... Is>(std::integer_sequence<int, Is...>) {
                 (seed(std::integral_constant<int, Is>{}), ...);
             }(std::make_integer_sequence<int, KL>{});
         };
-        if constexpr (V == 2 && VBF_W2_FIFO) {
-            // V = 2: the rounds as a rolled loop (one copy of the hashing code instead of RM: the
-            // unrolled four k = 19 rounds exceed the instruction cache), the stash a FIFO -- each
-            // round's KL indices enter at the top after the older ones move down KL slots, so every
-            // stash index stays static and the stash in registers
-#pragma unroll 1
-            for (uint32_t r = 0; r < (uint32_t)RM; ++r) {
-                uint32_t nw[KL];
-                round_body(r, r + 1 < (uint32_t)RM, [&](auto ic, uint32_t idx) { nw[decltype(ic)::value] = idx; });
-#pragma unroll
-                for (int i = 0; i + KL < RM * KL; ++i) stash[i] = stash[i + KL];
-#pragma unroll
-                for (int i = 0; i < KL; ++i) stash[RM * KL - KL + i] = nw[i];
-            }
-        } else {
-            auto round = [&](auto rc) {
-                constexpr int r = decltype(rc)::value;
-                const uint32_t slot = (uint32_t)r * kKeysPerRound + tid / SPL;
-                const uint32_t seed0 = (uint32_t)KL * (tid % SPL);
-                const bool valid = (uint32_t)r < pl.R && slot < nk;
-                Prefix p{};
-                if constexpr (PF) {
-                    const KeyHead h = head_cur;
-                    if constexpr (r + 1 < RM) head_cur = head_of(r + 1);
-                    if (valid) p = key_prefix_head<LP>(h);
-                } else if (valid) {
-                    if constexpr (FMT < 0) {
-                        uint64_t beg, len;
-                        key_span(slot, beg, len);
-                        p = key_prefix_at<LP>(dk.keys, beg, len);
-                    } else {
-                        p = key_prefix<FMT, LP>(dk, key_of(slot));
-                    }
-                }
-                SeedCtx q{};
-                if constexpr (FMT > 0) q = seed_ctx(p);
-                auto seed = [&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    uint32_t idx = kSentinel;
-                    if (valid && (SPL == 1 || seed0 + i < (uint32_t)K) && (KC == 0 || (uint32_t)i < pl.k)) {
-                        const uint64_t h = FMT > 0 ? seed_hash(q, seed0 + i) : prefix_hash(p, seed0 + i);
-                        idx = mod_m<M31, SAT>(h, pl.m, pl.mu);
-                        seg_count<C16, SB>(cnt0, idx);
-                    }
-                    stash[r * KL + i] = idx;
-                };
-                [&]<int... Is>(std::integer_sequence<int, Is...>) {
-                    (seed(std::integral_constant<int, Is>{}), ...);
-                }(std::make_integer_sequence<int, KL>{});
-            };
-            [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                (round(std::integral_constant<int, Rs>{}), ...);
-            }(std::make_integer_sequence<int, RM>{});
-        }
+        [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
+            (round(std::integral_constant<int, Rs>{}), ...);
+        }(std::make_integer_sequence<int, RM>{});
         ns = RM * KL;
     } else {
         ns = 0;
@@ -500,7 +328,7 @@ __global__ __launch_bounds__(V >= 1 ? 512 : kPBlock, V >= 1 ? 4 : 8) void k_tile
     __syncthreads();
     // run starts; the 512-thread shape scans up to 8 counters per thread where m > 2^31
     // (up to 4 096 segments)
-    constexpr int SPER = (V >= 1 && !M31) ? 8 : 4;
+    constexpr int SPER = (V == 1 && !M31) ? 8 : 4;
     auto gd_get = [&](uint32_t sg) -> uint32_t { return (gd[sg >> 1] >> ((sg & 1u) * 16)) & 0xFFFFu; };
     if constexpr (POS) {
         // every run padded to whole groups in HBM: gd = groups per segment (u16 pairs), scanned
@@ -527,15 +355,6 @@ __global__ __launch_bounds__(V >= 1 ? 512 : kPBlock, V >= 1 ? 4 : 8) void k_tile
     } else {
         block_exclusive_scan<false, SPER>(cnt, pl.nseg, wsum);
     }
-    constexpr uint32_t kNsMax = KK > 0 ? (uint32_t)(RMK * KL) : (uint32_t)kStash;
-    if constexpr (V == 2) {
-        __syncthreads();
-        tile_pack_windows<BS, SB>(pl, stash, ns, nk * (uint32_t)KK, cnt, cnt0, wsum, smem, lo,
-                                  tiles + (uint64_t)tile * pl.tile_words);
-        __syncthreads();
-        for (uint32_t sg = tid; sg < pl.nseg; sg += BS) ends[(uint64_t)sg * pl.ntS + tile] = (uint16_t)cnt[sg];
-        return;
-    }
     // the groups' nibble words start clear (ORed into below); the image held perm / staged keys
     // until the hashing rounds ended
     for (uint32_t g = tid; g < (POS ? pl.CPg : pl.CP) / 8; g += BS) smem[g * kGroupWords + 4] = 0;
@@ -548,6 +367,7 @@ __global__ __launch_bounds__(V >= 1 ? 512 : kPBlock, V >= 1 ? 4 : 8) void k_tile
     }
     // rank + place, 8 returning LDS atomics in flight before their results are used
     // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
+    constexpr uint32_t kNsMax = KK > 0 ? (uint32_t)(RMK * KL) : (uint32_t)kStash;
 #pragma unroll
     for (uint32_t t = 0; t < kNsMax; t += 8) {
         if (t >= ns) break;

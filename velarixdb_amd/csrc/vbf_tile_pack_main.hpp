@@ -14,10 +14,6 @@ hipError_t launch_main_fmt(const DevKeys& dk, const PartPlan& pl, uint32_t ntile
     const uint32_t k = pl.k;
     // m <= 2^31: the one-word remainder (fast_mod31); the runtime-k kernel keeps the general one
     auto pick = [&]<bool S>() {
-        if constexpr (S) {  // two placement windows (make_plan, VBF_K1W)
-            if (pl.k1v == 2 && k == 10) return k_tile_pack<FMT, LP, 10, true, false, 2>;
-            if (pl.k1v == 2 && k == 19) return k_tile_pack<FMT, LP, 19, true, false, 2>;
-        }
         if constexpr (FMT > 0 && S) {  // the 512-thread shape (make_plan: m <= 2^31)
             if (pl.k1v && k == 10) return pl.c16 ? k_tile_pack<FMT, LP, 10, true, true, 1>
                                                  : k_tile_pack<FMT, LP, 10, true, false, 1>;
@@ -42,7 +38,7 @@ hipError_t launch_main_fmt(const DevKeys& dk, const PartPlan& pl, uint32_t ntile
         err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)pl.lds1);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v >= 1 ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles, ends,
+    hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v == 1 ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles, ends,
                        (uint16_t*)nullptr);
     return hipGetLastError();
 }
