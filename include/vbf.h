@@ -244,9 +244,9 @@ int vbf_filter_busy(const vbf_filter* f);
  * counts as done, so it may call back into the library.  A child forked while a set is queued
  * does not run it: the child's next call on that filter returns VBF_EINVAL.  More generally, HIP
  * does not survive fork(): in a child of a process that used the GPU through the library, every
- * call on a device-resident filter (and creating one) returns VBF_EINVAL before any HIP call, and
- * freeing a handle there releases no device memory (it is the parent's); host-resident filters
- * work as usual. */
+ * call on a device-resident filter (and creating one) and every stateless device-pointer entry
+ * point returns VBF_EINVAL before any HIP call, and freeing a handle there releases no device
+ * memory (it is the parent's); host-resident filters work as usual. */
 int vbf_filter_stream_wait(const vbf_filter* f, void* stream);
 int vbf_filter_stream_record(vbf_filter* f, void* stream);
 /* contains over a batch (bf.rs:95-105): out[j] = 1 when every one of the k bits is set.

@@ -473,9 +473,11 @@ def test_forked_child_device_calls_fail_fast(vbf, ora):
     """A child forked from a process that used the GPU through the library (nothing queued) gets
     VBF_EINVAL ("forked") from every device-resident filter call instead of HIP calls that can
     hang or fault: a synchronous build, a queued set (its worker reports the failure at the next
-    drain), single-key contains (the host mirror is the parent's pinned memory), a words copy and
-    a new device filter.  Host-resident filters keep working in the child.  The parent is unaffected."""
+    drain), single-key contains (the host mirror is the parent's pinned memory), a words copy, a
+    new device filter and a stateless device-pointer call.  Host-resident filters keep working in
+    the child.  The parent is unaffected."""
     import os
+    from velarixdb_amd._lib import call
     from velarixdb_amd.filter import HOST
     from velarixdb_amd.keys import HostBatch
     n, L = 100_000, 16
@@ -494,6 +496,7 @@ def test_forked_child_device_calls_fail_fast(vbf, ora):
                 lambda: f.contains(bytes(h[:L])),
                 lambda: f.words(),
                 lambda: vbf.BloomFilter(0.01, 1000, device=f.device),
+                lambda: call("vbf_popcount_dev", None, 0, None, None),  # a stateless device entry point
             ]
             for i, p in enumerate(probes):
                 try:

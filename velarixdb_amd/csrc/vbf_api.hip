@@ -72,14 +72,32 @@ bool hip_forked() {
     return owner != 0 && owner != getpid();
 }
 
+// Records the calling process as the one that uses HIP (the first call wins); false in a child
+// forked from it.
+bool hip_owner() {
+    const pid_t me = getpid();
+    pid_t owner = 0;
+    return g_hip_pid.compare_exchange_strong(owner, me) || owner == me;
+}
+
+int fail_forked() {
+    return fail(VBF_EINVAL, "process %d forked from %d, which uses the GPU: HIP cannot be used in the child",
+                (int)getpid(), (int)g_hip_pid.load());
+}
+
+// The stateless device-pointer entry points (no DeviceGuard: they run on the caller's current
+// device) check the same at their start.
+#define FORK_GUARD()                          \
+    do {                                      \
+        if (!hip_owner()) return fail_forked(); \
+    } while (0)
+
 struct DeviceGuard {
     int prev = -1;
     hipError_t err = hipSuccess;
     bool forked = false;
     explicit DeviceGuard(int device) {
-        const pid_t me = getpid();
-        pid_t owner = 0;
-        if (!g_hip_pid.compare_exchange_strong(owner, me) && owner != me) {
+        if (!hip_owner()) {
             forked = true;
             err = hipErrorNotSupported;
             return;
@@ -96,9 +114,7 @@ struct DeviceGuard {
 
 #define DEVICE_SCOPE(dev)                                                                     \
     DeviceGuard guard_(dev);                                                                  \
-    if (guard_.forked)                                                                        \
-        return fail(VBF_EINVAL, "process %d forked from %d, which uses the GPU: HIP cannot be used " \
-                    "in the child", (int)getpid(), (int)g_hip_pid.load());                    \
+    if (guard_.forked) return fail_forked();                                                  \
     if (guard_.err != hipSuccess)                                                             \
         return fail(VBF_ENODEV, "hipSetDevice(%d): %s", (int)(dev), hipGetErrorString(guard_.err))
 
@@ -1081,8 +1097,7 @@ class AsyncQueue {
         {
             DeviceGuard g(s.device);
             if (g.forked) {
-                rc = fail(VBF_EINVAL, "process %d forked from %d, which uses the GPU: HIP cannot be used in the child",
-                          (int)getpid(), (int)g_hip_pid.load());
+                rc = fail_forked();
             } else if (g.err != hipSuccess) {
                 rc = fail(VBF_ENODEV, "hipSetDevice(%d): %s", s.device, hipGetErrorString(g.err));
             } else {
@@ -1148,6 +1163,7 @@ int vbf_profile_enable(int on) {
 }
 
 int vbf_profile_read(double* ms, uint64_t* launches, int nphases) {
+    FORK_GUARD();
     if (!ms || !launches || nphases < 0) return fail(VBF_EINVAL, "NULL argument");
     for (int i = 0; i < nphases; ++i) {
         ms[i] = 0.0;
@@ -1238,6 +1254,10 @@ uint64_t vbf_build_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
 
 int vbf_release_workspaces(void) {
     std::lock_guard<std::mutex> lk(g_ws_mu);
+    if (hip_forked()) {  // the parent's buffers: forget them, free nothing
+        g_ws.clear();
+        return ok();
+    }
     for (auto& w : g_ws) {
         int prev = -1;
         (void)hipGetDevice(&prev);
@@ -1252,6 +1272,7 @@ int vbf_release_workspaces(void) {
 
 int vbf_build_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                      int len_prefix, uint32_t m, uint32_t k, uint32_t* words, int strategy, void* stream) {
+    FORK_GUARD();
     int rc = check_mk(m, k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
@@ -1264,6 +1285,7 @@ int vbf_build_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stri
 int vbf_probe_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                      int len_prefix, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
                      int strategy, void* stream) {
+    FORK_GUARD();
     int rc = check_mk(m, k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
@@ -1282,6 +1304,7 @@ int vbf_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
 int vbf_probe_count_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                            int len_prefix, uint32_t m, uint32_t k, const uint32_t* words,
                            unsigned long long* count_dev, int strategy, void* stream) {
+    FORK_GUARD();
     int rc = check_mk(m, k, n);
     if (rc) return rc;
     if ((rc = check_keys(keys, offsets, stride, n))) return rc;
@@ -1300,6 +1323,7 @@ int vbf_probe_count_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t s
 
 int vbf_hashes_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                    int len_prefix, uint32_t k, uint64_t* out, void* stream) {
+    FORK_GUARD();
     int rc = check_keys(keys, offsets, stride, n);
     if (rc) return rc;
     if (n && k && !out) return fail(VBF_EINVAL, "out is NULL");
@@ -1309,18 +1333,21 @@ int vbf_hashes_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
 }
 
 int vbf_or_words_dev(uint32_t* dst, const uint32_t* src, uint64_t nwords, void* stream) {
+    FORK_GUARD();
     if (nwords && (!dst || !src)) return fail(VBF_EINVAL, "NULL words");
     HIP_TRY(vbf::launch_or_words(dst, src, nwords, (hipStream_t)stream));
     return ok();
 }
 
 int vbf_popcount_dev(const uint32_t* words, uint64_t nwords, unsigned long long* count_dev, void* stream) {
+    FORK_GUARD();
     if (!count_dev || (nwords && !words)) return fail(VBF_EINVAL, "NULL argument");
     HIP_TRY(vbf::launch_popcount(words, nwords, count_dev, (hipStream_t)stream));
     return ok();
 }
 
 int vbf_gen_fixed_dev(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* out, void* stream) {
+    FORK_GUARD();
     if (n && len && !out) return fail(VBF_EINVAL, "out is NULL");
     HIP_TRY(vbf::launch_gen_fixed(seed, base, n, len, out, (hipStream_t)stream));
     return ok();
@@ -1328,6 +1355,7 @@ int vbf_gen_fixed_dev(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, ui
 
 int vbf_gen_var_dev(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* offsets, uint8_t* out,
                     void* stream) {
+    FORK_GUARD();
     if (n && (!offsets || !out)) return fail(VBF_EINVAL, "NULL argument");
     HIP_TRY(vbf::launch_gen_var(seed, base, n, offsets, out, (hipStream_t)stream));
     return ok();
@@ -1335,6 +1363,7 @@ int vbf_gen_var_dev(uint64_t seed, uint64_t base, uint64_t n, const uint64_t* of
 
 int vbf_gen_sst_fixed_dev(uint64_t seed, uint64_t base, uint64_t n, uint32_t len, uint8_t* data,
                           uint32_t* blocks, void* stream) {
+    FORK_GUARD();
     if (n && (!data || !blocks)) return fail(VBF_EINVAL, "NULL argument");
     if (len + 17 > 4096) return fail(VBF_EINVAL, "an entry of %u + 17 bytes exceeds a 4096-byte block", len);
     HIP_TRY(vbf::gen_sst_fixed(seed, base, n, len, data, blocks, (hipStream_t)stream));
@@ -2076,6 +2105,7 @@ int vbf_sst_index_blocks(const uint8_t* index, uint64_t len, uint32_t* offsets, 
 int vbf_sst_decode_dev(const uint8_t* data, uint64_t len, const uint32_t* blocks, uint64_t nblocks, uint8_t* keys,
                        uint64_t keys_cap, uint64_t* offsets, uint32_t* val_offsets, uint64_t* created_ms,
                        uint8_t* tombstones, uint64_t entries_cap, uint64_t* n_out, void* stream) {
+    FORK_GUARD();
     if (!n_out) return fail(VBF_EINVAL, "n_out is NULL");
     hipStream_t s = (hipStream_t)stream;
     vbf::SstArgs a;
@@ -2432,6 +2462,7 @@ extern "C" {
 int vbf_multi_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n, int len_prefix,
                         uint32_t nsst, const vbf_filter* const* filters, const uint8_t* bounds,
                         const uint64_t* bounds_off, uint8_t* out, void* stream) {
+    FORK_GUARD();
     int rc = check_keys(keys, offsets, stride, n);
     if (rc) return rc;
     if (nsst && filters && filters[0]) {
@@ -2759,6 +2790,7 @@ int vbf_compact_merge_dev(const uint8_t* keys, const uint64_t* offsets, const in
                           const uint64_t* map_off, const int64_t* map_time, uint64_t map_n, int use_ttl,
                           uint64_t entry_ttl_ms, uint64_t tombstone_ttl_ms, uint64_t now_ms, uint32_t* out_ids,
                           uint64_t* n_out, uint32_t* upd_ids, int64_t* upd_time, uint64_t* n_upd, void* stream) {
+    FORK_GUARD();
     int rc = compact_merge(keys, offsets, created_ms, tombstones, run_off, nruns, map_keys, map_off, map_time, map_n,
                            use_ttl, entry_ttl_ms, tombstone_ttl_ms, now_ms, out_ids, n_out, upd_ids, upd_time, n_upd,
                            (hipStream_t)stream);
@@ -2769,6 +2801,7 @@ int vbf_gather_entries_dev(const uint8_t* keys, const uint64_t* offsets, const i
                            const uint8_t* tombstones, const uint32_t* val_offsets, const uint32_t* ids, uint64_t n,
                            uint8_t* out_keys, uint64_t out_keys_cap, uint64_t* out_offsets, int64_t* out_created_ms,
                            uint8_t* out_tombstones, uint32_t* out_val_offsets, uint64_t* key_bytes, void* stream) {
+    FORK_GUARD();
     int rc = gather_entries(keys, offsets, created_ms, tombstones, val_offsets, ids, n, out_keys, out_keys_cap,
                             out_offsets, out_created_ms, out_tombstones, out_val_offsets, key_bytes, (hipStream_t)stream);
     return rc ? rc : ok();
