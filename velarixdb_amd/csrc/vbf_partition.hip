@@ -552,10 +552,13 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     // workgroup, e.g. > 80 KiB to hold one workgroup per CU
     static const int lds_min = [] { const char* e = getenv("VBF_TILE_LDS_MIN"); return e ? atoi(e) : 0; }();
     if (lds_min > 0) pl.lds1 = std::max<uint32_t>(pl.lds1, std::min<uint32_t>((uint32_t)lds_min, kLdsPerCu));
-    // stagger the second resident workgroup per CU by ~half a tile of hashing (~25 us at k=10,
-    // ~3000 keys): s_sleep 127 = 8128 cycles, ~3.7 us.  VBF_STAGGER=0 disables (A/B).
+    // VBF_STAGGER = n (A/B): the second resident workgroup per CU starts n x s_sleep 127 (8128
+    // cycles, ~3.7 us) later.  Off by default since round 5: with the current kernels 0 measured
+    // best at k = 10 and 19 (monotonic over 0..14, two passes; configs 3 / 5 within noise,
+    // profiles/r05/stagger_r5.txt, stagger_cfg_r5.txt) -- the workgroups fall out of step by
+    // themselves after the first tile.
     static const int env = [] { const char* e = getenv("VBF_STAGGER"); return e ? atoi(e) : -1; }();
-    const uint32_t sleeps = env >= 0 ? (uint32_t)env : 7;
+    const uint32_t sleeps = env >= 0 ? (uint32_t)env : 0;
     pl.stagger_lo = 256;
     pl.stagger_hi = 512;
     pl.stagger_sleeps = sleeps;

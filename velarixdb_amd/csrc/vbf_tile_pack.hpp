@@ -181,9 +181,9 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     uint32_t* smem = gd + pl.gd_words;                  // the image: (cnt_words + 48) * 4 % 16 == 0
     uint16_t* lo = reinterpret_cast<uint16_t*>(smem);  // before placement: perm (offsets layout)
     const uint32_t tid = threadIdx.x;
-    // Stagger (speed only): the second workgroup dispatched to each CU starts ~half a tile
-    // later, so the two co-resident workgroups alternate hashing (VALU) and sorting (LDS)
-    // instead of contending for the same pipe at the same time.
+    // Stagger (VBF_STAGGER, speed only, off by default since round 5): the second workgroup
+    // dispatched to each CU may start a few s_sleeps later, so the two co-resident workgroups
+    // alternate hashing (VALU) and sorting (LDS) from the first tile on.
     if (blockIdx.x >= pl.stagger_lo && blockIdx.x < pl.stagger_hi) {
         for (uint32_t i = 0; i < pl.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
     }
