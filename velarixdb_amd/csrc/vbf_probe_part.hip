@@ -1,6 +1,7 @@
 // vbf_probe_part.hip -- the partitioned probe (contains() for large batches): the build's
 // tile/segment scheme (vbf_partition.hip) applied to lookups.
-#include "vbf_tile_pack.hpp"
+#include "vbf_probe_pack.hpp"
+#include "vbf_tile_pack_rk.hpp"
 
 namespace vbf {
 
@@ -17,113 +18,6 @@ namespace vbf {
 //                     the answer byte (or count the hits).
 // Without early exit every key costs k hashes, but no probe leaves the chip's LDS.
 // =================================================================================================
-constexpr uint32_t kOffMask = (1u << kSegBits) - 1;
-static_assert(kSegBits == 20, "probe entries hold a 12-bit key id above the 20-bit offset");
-
-// SB: segment = 2^SB filter positions (bits of one filter: 20; bytes of an interleaved group of
-// filters, vbf_multi_part.hip: 17).  An entry is (tile-local key id << SB) | offset in segment.
-// SAT: m == 2^32 - 1, remainders by mod_sat (sip13.hpp).
-// Per segment one LDS word holds the run's count (-> start -> end) in its low half and its padded
-// start in the high half: both stay below 2^16 (C + 7 * nseg <= cap <= 65535, probe_partition_
-// supported), so one scan of the words scans both and no half carries into the other -- half the
-// counters' LDS of two u32 arrays, which at m = 2^32 - 1 (4 096 segments) buys 33 % larger tiles.
-template <int FMT, bool LP, int K, bool M31, int SB, bool SAT = false>
-__global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan pl, uint32_t* tiles, uint16_t* ends) {
-    constexpr uint32_t kOff = (1u << SB) - 1;
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    uint32_t* ent = smem;               // C entries
-    uint32_t* cnt = ent + pl.C;         // nseg_pad: count | padded count << 16 -> starts -> end | padded start
-    uint32_t* wsum = cnt + pl.nseg_pad; // 16
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] = 0;
-    __syncthreads();
-    uint32_t stash[kStash];
-    const uint64_t key0 = (uint64_t)blockIdx.x * pl.KT;
-    const uint64_t key_end = std::min<uint64_t>(dk.n, key0 + pl.KT);
-    uint32_t ns;
-    if constexpr (K > 0) {
-        constexpr int RM = rounds_max(K);
-        // compile-time r per round (see k_tile_pack): keeps the stash out of scratch memory
-        auto round = [&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
-            const bool valid = (uint32_t)r < pl.R && j < key_end;
-            Prefix p{};
-            if (valid) p = key_prefix<FMT, LP>(dk, j);
-            SeedCtx q{};
-            if constexpr (FMT > 0) q = seed_ctx(p);  // block-aligned prefix: seed_hash (sip13.hpp)
-            // the seed slots as a fold with a compile-time slot number, as in k_tile_pack
-            auto seed = [&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                uint32_t idx = kSentinel;
-                if (valid) {
-                    idx = mod_m<M31, SAT>(FMT > 0 ? seed_hash(q, i) : prefix_hash(p, i), pl.m, pl.mu);
-                    atomicAdd(&cnt[idx >> SB], 1u);
-                }
-                stash[r * K + i] = idx;
-            };
-            [&]<int... Is>(std::integer_sequence<int, Is...>) {
-                (seed(std::integral_constant<int, Is>{}), ...);
-            }(std::make_integer_sequence<int, K>{});
-        };
-        [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-            (round(std::integral_constant<int, Rs>{}), ...);
-        }(std::make_integer_sequence<int, RM>{});
-        ns = RM * K;
-    } else {
-        ns = 0;
-        for (uint32_t r = 0; r < pl.R; ++r) {
-            const uint64_t j = key0 + (uint64_t)r * kPBlock + tid;
-            const bool valid = j < key_end;
-            Prefix p{};
-            if (valid) p = key_prefix<FMT, LP>(dk, j);
-            for (uint32_t i = 0; i < pl.k; ++i) {
-                uint32_t idx = kSentinel;
-                if (valid) {
-                    idx = mod_m<M31>(prefix_hash(p, i), pl.m, pl.mu);
-                    atomicAdd(&cnt[idx >> SB], 1u);
-                }
-                stash[ns++] = idx;
-            }
-        }
-    }
-    __syncthreads();
-    for (uint32_t s = tid; s < pl.nseg; s += kPBlock) cnt[s] |= ((cnt[s] + 7) & ~7u) << 16;
-    __syncthreads();
-    block_exclusive_scan(cnt, pl.nseg, wsum);
-    __syncthreads();
-    const uint32_t per = K > 0 ? (uint32_t)K : pl.k;
-    // the bound is a compile-time constant for K > 0 (ns == RM * K); K == 0 stops at ns
-    constexpr uint32_t kNsMax = K > 0 ? (uint32_t)(rounds_max(K) * K) : (uint32_t)kStash;
-#pragma unroll
-    for (uint32_t t = 0; t < kNsMax; t += 8) {
-        if (t >= ns) break;
-        uint32_t pos[8], val[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? atomicAdd(&cnt[val[q] >> SB], 1u) & 0xFFFFu : 0u;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if (val[q] != kSentinel) {
-                const uint32_t local = ((t + q) / per) * kPBlock + tid;  // round r = slot / k
-                ent[pos[q]] = (local << SB) | (val[q] & kOff);
-            }
-    }
-    __syncthreads();
-    // runs -> global, padded to multiples of 8; 8-lane groups, one run at a time
-    const uint32_t grp = tid >> 3, q = tid & 7;
-    uint32_t* out = tiles + (uint64_t)blockIdx.x * pl.cap;
-    uint16_t* eo = ends + (uint64_t)blockIdx.x * pl.nseg;
-    for (uint32_t s = grp; s < pl.nseg; s += kPBlock / 8) {
-        const uint32_t st = s ? cnt[s - 1] & 0xFFFFu : 0, en = cnt[s] & 0xFFFFu, c = en - st, pc = (c + 7) & ~7u;
-        const uint32_t d = cnt[s] >> 16;
-        for (uint32_t x = q; x < pc; x += 8) out[d + x] = ent[std::min(st + x, en - 1)];
-        if (q == 0) eo[s] = (uint16_t)(d + pc);
-    }
-}
-
 // Q3 variants (VBF_Q3, speed only; identical answers):
 //   0: one pass per 8-lane group and tile, 8 tiles per wave-step
 //   1: the k_seg_or<3> scheme -- a wave serves 8 * NG tiles per batch, run bounds loaded
@@ -584,7 +478,10 @@ ProbePlan make_probe_plan(uint32_t m, uint32_t k, int sb) {
     pl.nwords = ((uint64_t)m + 31) / 32;
     pl.nseg = (uint32_t)(((uint64_t)m + (1u << sb) - 1) >> sb);
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
-    const uint32_t rmax = (uint32_t)rounds_max((int)k);
+    // k outside {4, 10, 19} on 2^20-bit segments: the runtime-k class kernel's rounds (its stash holds
+    // rounds_max(class) rounds of class slots; the scratch-stash kernel runs any round count)
+    const uint32_t kc = (sb == kSegBits && k != 4 && k != 10 && k != 19) ? tile_pack_class(k) : 0u;
+    const uint32_t rmax = (uint32_t)rounds_max((int)(kc ? kc : k));
     const int64_t avail = (int64_t)(kLdsPerCu / 2) - 64 - 4 * (int64_t)pl.nseg_pad;
     const int64_t kt = std::min<int64_t>(std::min<int64_t>((int64_t)rmax * kPBlock, avail / 4 / k), 4096);
     pl.KT = (uint32_t)std::max<int64_t>(kt, 1);
@@ -630,6 +527,14 @@ hipError_t launch_probe_pack_fmt(const DevKeys& dk, const ProbePlan& pl, uint32_
              : k == 19 ? k_probe_pack<FMT, LP, 19, S, SB>  // the reference's default p = 1e-4
                        : k_probe_pack<FMT, LP, 0, false, SB>;
     };
+    if constexpr (LP && SB == kSegBits) {
+        // k outside the compiled set: the runtime-k class kernels (register stash) -- unless
+        // VBF_KCLASS=0 keeps the scratch-stash kernel (A/B)
+        static const int kcls = [] { const char* e = getenv("VBF_KCLASS"); return e ? atoi(e) : 1; }();
+        const uint32_t kc = (k != 4 && k != 10 && k != 19 && kcls != 0) ? tile_pack_class(k) : 0u;
+        if (kc) return kc <= 12 ? launch_probe_pack_class_a(FMT, kc, dk, pl, ntiles, tiles, ends, s)
+                                : launch_probe_pack_class_b(FMT, kc, dk, pl, ntiles, tiles, ends, s);
+    }
     auto fn = pl.m <= (1ull << 31) ? pick.template operator()<true>() : pick.template operator()<false>();
     if constexpr (LP && SB == kSegBits) {  // m = 2^32 - 1 (the reference's saturated size): SAT kernels
         if (pl.m == 0xFFFFFFFFull && (k == 4 || k == 10 || k == 19))
