@@ -1,8 +1,8 @@
 """GPU parity for the partitioned probe (contains(), bf.rs:95-105, for large batches): its
 answers equal the per-key early-exit probe and the oracle, bit for bit, across key layouts,
 filter sizes (one segment, a few, thousands, the u32-saturated config-5 size) and k values
-(compile-time 4/10/19 and run-time k: the class packs with a register stash for keys with the
-length prefix, the scratch-stash pack for the rest)."""
+(compile-time 4/10/19 and run-time k: the class packs with a register stash, with and without
+the length prefix)."""
 import ctypes
 
 import numpy as np
@@ -29,6 +29,8 @@ CASES = [  # (L or None for var-length, len_prefix, m, k, n)
     # fixed and variable-length keys
     (None, 1, 300_000_007, 14, 400_000), (16, 1, 200_000_003, 23, 300_000), (32, 1, 50_000_017, 12, 400_000),
     (8, 1, 40_000_003, 32, 200_000), (16, 1, 100_000_007, 21, 300_000), (None, 1, 2_500_000_001, 7, 300_000),
+    # ... and for keys hashed without the length prefix (pre-encoded integer keys)
+    (16, 0, 100_000_007, 14, 300_000), (None, 0, 300_000_007, 23, 300_000), (8, 0, 3_000_000_017, 5, 400_000),
 ]
 
 

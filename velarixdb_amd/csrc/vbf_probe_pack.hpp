@@ -118,33 +118,39 @@ __global__ __launch_bounds__(kPBlock, 8) void k_probe_pack(DevKeys dk, ProbePlan
     }
 }
 
-// The runtime-k class probe packs (vbf_probe_part_rk_a.hip: classes 5, 8, 12; _b: 16, 21, 24, 32),
-// keys hashed with the length prefix, 2^20-bit segments; hipErrorNotSupported for other shapes.
+// The runtime-k class probe packs on 2^20-bit segments: vbf_probe_part_rk_a.hip (classes 5, 8, 12)
+// and _b (16, 21, 24, 32) for keys hashed with the length prefix, _c / _d the same without it (the
+// pre-encoded integer keys of bf.rs:275-424); hipErrorNotSupported for other shapes.
 hipError_t launch_probe_pack_class_a(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
                                      uint32_t* tiles, uint16_t* ends, hipStream_t s);
 hipError_t launch_probe_pack_class_b(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
                                      uint32_t* tiles, uint16_t* ends, hipStream_t s);
+hipError_t launch_probe_pack_class_c(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
+                                     uint32_t* tiles, uint16_t* ends, hipStream_t s);
+hipError_t launch_probe_pack_class_d(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
+                                     uint32_t* tiles, uint16_t* ends, hipStream_t s);
 
 // One class kernel: m <= 2^31 takes the one-word remainder, above it the general one.
-template <int FMT, int KC>
+template <int FMT, bool LP, int KC>
 hipError_t launch_probe_pack_one_class(const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles, uint32_t* tiles,
                                        uint16_t* ends, hipStream_t s) {
-    auto fn = pl.m <= (1ull << 31) ? k_probe_pack<FMT, true, 0, true, kSegBits, false, KC>
-                                   : k_probe_pack<FMT, true, 0, false, kSegBits, false, KC>;
+    auto fn = pl.m <= (1ull << 31) ? k_probe_pack<FMT, LP, 0, true, kSegBits, false, KC>
+                                   : k_probe_pack<FMT, LP, 0, false, kSegBits, false, KC>;
     hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)pl.lds1);
     if (err == hipSuccess) hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
     return err;
 }
 
-template <int... KCs>
+template <bool LPC, int... KCs>
 hipError_t launch_probe_pack_classes(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
                                      uint32_t* tiles, uint16_t* ends, hipStream_t s) {
     hipError_t err = hipErrorNotSupported;
-    with_fmt(fmt, true, [&]<int FMT, bool LP>() {
-        ((kc == (uint32_t)KCs ? (void)(err = launch_probe_pack_one_class<FMT, KCs>(dk, pl, ntiles, tiles, ends, s))
-                              : (void)0),
-         ...);
+    with_fmt(fmt, LPC, [&]<int FMT, bool LP>() {
+        if constexpr (LP == LPC)
+            ((kc == (uint32_t)KCs ? (void)(err = launch_probe_pack_one_class<FMT, LP, KCs>(dk, pl, ntiles, tiles, ends, s))
+                                  : (void)0),
+             ...);
     });
     return err;
 }

@@ -527,13 +527,19 @@ hipError_t launch_probe_pack_fmt(const DevKeys& dk, const ProbePlan& pl, uint32_
              : k == 19 ? k_probe_pack<FMT, LP, 19, S, SB>  // the reference's default p = 1e-4
                        : k_probe_pack<FMT, LP, 0, false, SB>;
     };
-    if constexpr (LP && SB == kSegBits) {
+    if constexpr (SB == kSegBits) {
         // k outside the compiled set: the runtime-k class kernels (register stash) -- unless
         // VBF_KCLASS=0 keeps the scratch-stash kernel (A/B)
         static const int kcls = [] { const char* e = getenv("VBF_KCLASS"); return e ? atoi(e) : 1; }();
         const uint32_t kc = (k != 4 && k != 10 && k != 19 && kcls != 0) ? tile_pack_class(k) : 0u;
-        if (kc) return kc <= 12 ? launch_probe_pack_class_a(FMT, kc, dk, pl, ntiles, tiles, ends, s)
+        if (kc) {
+            if constexpr (LP)
+                return kc <= 12 ? launch_probe_pack_class_a(FMT, kc, dk, pl, ntiles, tiles, ends, s)
                                 : launch_probe_pack_class_b(FMT, kc, dk, pl, ntiles, tiles, ends, s);
+            else
+                return kc <= 12 ? launch_probe_pack_class_c(FMT, kc, dk, pl, ntiles, tiles, ends, s)
+                                : launch_probe_pack_class_d(FMT, kc, dk, pl, ntiles, tiles, ends, s);
+        }
     }
     auto fn = pl.m <= (1ull << 31) ? pick.template operator()<true>() : pick.template operator()<false>();
     if constexpr (LP && SB == kSegBits) {  // m = 2^32 - 1 (the reference's saturated size): SAT kernels
