@@ -1,6 +1,6 @@
 // vbf_probe_pack.hpp -- Q1 of the partitioned probe (k_probe_pack), shared by vbf_probe_part.hip (the
-// compiled k and the scratch-stash kernel) and vbf_probe_part_rk_{a,b}.hip (the runtime-k classes,
-// translation units of their own so the library builds in parallel).
+// compiled k and the scratch-stash kernel) and vbf_probe_part_rk_{a,b,c,d}.hip (the runtime-k
+// classes, translation units of their own so the library builds in parallel).
 #pragma once
 #include "vbf_tile_pack.hpp"
 
