@@ -43,6 +43,8 @@ def make_parser():
                     help="configs 2/4: hash the keys without the length prefix (len_prefix = 0: pre-encoded "
                          "integer keys such as bf.rs:307-424's usize keys)")
     ap.add_argument("--neg-keys", type=int, default=None)
+    ap.add_argument("--probe-ab", action="store_true",
+                    help="config 5: also time the positive sweep on the round-3 probe pipeline (VBF_PROBE_PU=0)")
     ap.add_argument("--e2e", action="store_true")
     ap.add_argument("--e2e-fresh-out", action="store_true", help="--e2e: a fresh host array per step")
     ap.add_argument("--sst", action="store_true", help="SST data.db decode + rebuild (8(f) row 2)")
@@ -591,12 +593,41 @@ def bench_cfg5(ctx, args):
 
     wall, kms, phases = timed_steps(ctx, step, args.steps, args.warmup)
     cnt = torch.zeros(1, dtype=torch.int64, device=ctx.dev)
-    t0 = time.perf_counter()
-    call("vbf_probe_count_dev", vp(keys), None, L, n, 1, m, k, vp(buf), vp(cnt), ctx.sp)
-    torch.cuda.synchronize()
-    sweep = ctx.max_over_ranks(time.perf_counter() - t0)
-    hits = int(ctx.sum_over_ranks(int(cnt.item())))
-    assert hits == N, "positive sweep found %d of %d" % (hits, N)
+
+    # the full positive sweep (contains() of every key, bf.rs:95-105): one untimed call (the AUTO
+    # strategy's hit-rate sample, workspace allocation), then `reps` timed calls with the library's
+    # per-phase hipEvents; every call must find all N keys.  Also timed: the round-3 pipeline
+    # (VBF_PROBE_PU=0, read per call) for the A/B record.
+    from velarixdb_amd._lib import lib, profile_read
+
+    def sweep_once():
+        cnt.zero_()
+        call("vbf_probe_count_dev", vp(keys), None, L, n, 1, m, k, vp(buf), vp(cnt), ctx.sp)
+
+    def timed_sweeps(reps=3):
+        sweep_once()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        lib.vbf_profile_enable(1)
+        profile_read()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sweep_once()
+        torch.cuda.synchronize()
+        dt = ctx.max_over_ranks((time.perf_counter() - t0) / reps)
+        lib.vbf_profile_enable(0)
+        hits = int(ctx.sum_over_ranks(int(cnt.item())))
+        assert hits == N, "positive sweep found %d of %d" % (hits, N)
+        return dt, phase_report(profile_read(), reps)
+
+    sweep, sweep_phases = timed_sweeps()
+    sweep_r3 = None
+    if args.probe_ab:
+        os.environ["VBF_PROBE_PU"] = "0"
+        try:
+            sweep_r3, _ = timed_sweeps()
+        finally:
+            os.environ.pop("VBF_PROBE_PU", None)
     nn = args.neg_keys
     nk = torch.empty(nn * L, dtype=torch.uint8, device=ctx.dev)
     call("vbf_gen_fixed_dev", wl.SEED_CFG5 ^ 0xFF, N + ctx.rank * nn, nn, L, vp(nk), ctx.sp)
@@ -628,6 +659,8 @@ def bench_cfg5(ctx, args):
         "vs_baseline": None, "dtype": "u64", "data": "synthetic", "key_gib_per_s": value * L / 2**30,
         "config": {"workload": "config5: %d x 32B keys, 15 bits/key -> m=%d (u32-saturated), k=%d; OR all-reduce over %d ranks" % (N, m, k, ctx.world)},
         "build_kernel_ms": float(np.mean(kms)), "roofline": roofline, "probe_sweep_keys_per_s": N / sweep,
+        "probe_sweep_ms": sweep * 1e3, "probe_sweep_phases": sweep_phases,
+        "probe_sweep_ms_round3_pipeline": None if sweep_r3 is None else sweep_r3 * 1e3,
         "negatives": {"n": nn * ctx.world, "false_positives": fp, "fpr": fp / (nn * ctx.world)},
     }
 

@@ -140,6 +140,12 @@ int vbf_hashes_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride
                    int len_prefix, uint32_t k, uint64_t* out, void* stream);
 /* dst |= src over nwords (16-byte aligned): merging partial filters of one key set. */
 int vbf_or_words_dev(uint32_t* dst, const uint32_t* src, uint64_t nwords, void* stream);
+/* dst[i] = OR over p < nparts of src[p * part_stride + i], i < nwords, in one pass (the fold of the
+ * multi-GPU OR all-reduce: every rank's copy of one bit range, received back to back; the bitwise
+ * OR that merges partial filters of one key set, bf.rs:89).  16-byte aligned pointers, part_stride
+ * a multiple of 4 words and >= nwords; dst may be src (part 0) itself. */
+int vbf_or_fold_dev(uint32_t* dst, const uint32_t* src, uint64_t nwords, uint32_t nparts, uint64_t part_stride,
+                    void* stream);
 /* *count_dev += popcount(words[0..nwords)). */
 int vbf_popcount_dev(const uint32_t* words, uint64_t nwords, unsigned long long* count_dev,
                      void* stream);
@@ -265,6 +271,10 @@ uint32_t vbf_filter_num_elements(const vbf_filter* f);       /* bf.rs:198-201 */
 uint32_t vbf_filter_num_hash_functions(const vbf_filter* f); /* bf.rs:210-213 */
 double vbf_filter_false_positive_rate(const vbf_filter* f);  /* bf.rs:54 */
 int vbf_filter_device(const vbf_filter* f);          /* a device id or VBF_DEVICE_HOST */
+/* Bytes of host memory the filter's bits hold: the host-resident words (allocated on their first
+ * use, so a filter created on the host and migrated to a GPU before any set -- the compaction
+ * filter of compactors/sized.rs:192-193 -- holds none) plus a device filter's pinned host mirror. */
+uint64_t vbf_filter_host_bytes(const vbf_filter* f);
 uint32_t* vbf_filter_words_dev(const vbf_filter* f); /* device pointer to the bit array (NULL if host) */
 /* Read-only device pointer to the bit array (NULL if host-resident), e.g. the source of an OR
  * merge: unlike vbf_filter_words_dev it does not mark the bits externally written, so the host

@@ -1,5 +1,7 @@
 #!/bin/bash
-# GPU-box session: smoke, parity tests, bench, rocprofv3 kernel-trace summary.
+# GPU-box session, parameterised by STEPS (the one script for every lease; round 5's one-off
+# tools/r5_*.sh are folded in as the steps suite / measure / bench5ab / sel):
+#   STEPS="smoke pytest bench prof" (default) ... see the case list below.
 # Every GPU step has its own time limit; the script stops at the first fault/abort/timeout.
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -23,6 +25,23 @@ run() {  # run NAME SECONDS CMD...
 
 for s in $STEPS; do
   case $s in
+    suite)  run suite 1200 python -u -m pytest tests/ -x -v -m gpu --timeout 900 --timeout-method thread ;;
+    measure)  # bench line, kernel stats (k = 10, 19), SQ / FETCH_SIZE / WRITE_SIZE passes per config
+        B="python3 $ROOT/bench.py --no-cpu-baseline"
+        SQ="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+        run bench_default 420 python3 bench.py
+        (cd /tmp && run prof10 300 rocprofv3 --kernel-trace --stats -d "$OUT/meas/prof10" -o run --output-format csv -- $B --steps 40 --warmup 5) || exit $?
+        (cd /tmp && run prof19 300 rocprofv3 --kernel-trace --stats -d "$OUT/meas/prof19" -o run --output-format csv -- $B --steps 20 --warmup 3 --bits-per-key 19) || exit $?
+        i=0
+        for a in "--steps 3 --warmup 1" "--steps 3 --warmup 1 --bits-per-key 19" "--config 3 --steps 3 --warmup 1" "--config 5 --steps 2 --warmup 1"; do
+          i=$((i+1))
+          for c in "$SQ" FETCH_SIZE WRITE_SIZE; do
+            tag=$(echo "$c" | cut -c1-5)
+            (cd /tmp && run pmc_${tag}_$i 240 rocprofv3 --pmc $c -d "$OUT/meas/${tag}_$i" -o run --output-format csv -- $B $a) || exit $?
+          done
+        done ;;
+    sel)    run pytest_sel 1200 python -u -m pytest $PYTEST_ARGS -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    bench5ab) run bench_cfg5_ab 900 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline --probe-ab ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     pytest) run pytest_gpu 1200 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     bench)  run bench 600 python bench.py ;;

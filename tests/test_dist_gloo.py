@@ -28,7 +28,7 @@ def _worker(rank, world, port, m, k, n, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import oracle
-        from velarixdb_amd.dist import or_allreduce_, padded_words, shard_range
+        from velarixdb_amd.dist import or_allreduce_, or_fold_host, padded_words, shard_range
         from velarixdb_amd.keys import HostBatch
         lo, hi = shard_range(n, rank, world)
         keys = oracle.gen_fixed(0x5EED0005, lo, hi - lo, 32)
@@ -36,8 +36,14 @@ def _worker(rank, world, port, m, k, n, q):
         nwords = (m + 31) // 32
         buf, chunk = padded_words(nwords, world, "cpu")
         buf[:nwords] = torch.from_numpy(partial.view(np.int32))
-        or_allreduce_(buf, chunk, or_into=lambda a, b: a.bitwise_or_(b))  # gloo: CPU tensors
-        q.put((rank, buf[:nwords].numpy().view(np.uint32).copy(), buf[nwords:].abs().sum().item()))
+        or_allreduce_(buf, chunk, fold=or_fold_host)  # gloo: CPU tensors
+        first = buf[:nwords].numpy().view(np.uint32).copy()
+        # a second call reuses the receive workspace: the result must not depend on its contents
+        buf[:nwords] = torch.from_numpy(partial.view(np.int32))
+        buf[nwords:] = 0
+        or_allreduce_(buf, chunk)  # the default fold for CPU tensors
+        assert np.array_equal(first, buf[:nwords].numpy().view(np.uint32))
+        q.put((rank, first, buf[nwords:].abs().sum().item()))
     finally:
         dist.destroy_process_group()
 

@@ -756,6 +756,37 @@ def test_or_words_kernel(vbf):
         or_words_dev(torch.zeros(4, dtype=torch.int32), torch.zeros(4, dtype=torch.int32))
 
 
+def test_or_fold_kernel(vbf):
+    """vbf_or_fold_dev (dist.or_fold_dev: the one-pass fold of the multi-GPU OR all-reduce, VERDICT
+    r05 #7): the OR of 1..8 back-to-back parts, into a separate buffer and in place into part 0,
+    ragged lengths (the words past a multiple of 4 take the scalar tail); misaligned pointers,
+    an unaligned stride and overlapping parts are refused."""
+    from velarixdb_amd.dist import or_fold_dev
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    for parts in (1, 2, 3, 8):
+        for chunk in (4, 1024, (1 << 18) + 4):
+            src = torch.randint(-2**31, 2**31 - 1, (parts * chunk,), dtype=torch.int32, device=DEV, generator=g)
+            want = src[:chunk].clone()
+            for p in range(1, parts):
+                want |= src[p * chunk:(p + 1) * chunk]
+            out = torch.full((chunk,), 0x5A5A5A5A, dtype=torch.int32, device=DEV)
+            or_fold_dev(out, src, parts, chunk)
+            or_fold_dev(src[:chunk], src, parts, chunk)  # in place, as or_allreduce_ runs it
+            torch.cuda.synchronize()
+            assert torch.equal(out, want) and torch.equal(src[:chunk], want), (parts, chunk)
+    # nwords not a multiple of 4 (the tail loop), parts 8 words apart
+    src = torch.randint(-2**31, 2**31 - 1, (24,), dtype=torch.int32, device=DEV, generator=g)
+    out = torch.zeros(8, dtype=torch.int32, device=DEV)
+    vbf._lib.call("vbf_or_fold_dev", _ptr(out), _ptr(src), 7, 3, 8, _stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out[:7], (src[0:8] | src[8:16] | src[16:24])[:7]) and int(out[7]) == 0
+    a = torch.zeros(40, dtype=torch.int32, device=DEV)
+    for args in ((_ptr(a[1:]), _ptr(a[8:]), 8, 2, 8), (_ptr(a), _ptr(a[8:]), 8, 2, 10), (_ptr(a), _ptr(a[8:]), 8, 2, 4)):
+        with pytest.raises(vbf.VbfError):
+            vbf._lib.call("vbf_or_fold_dev", *args, _stream())
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,m,k,strategy", [
     (200_000, 600_000_000, 10, PARTITIONED),  # one workgroup per segment: the fused path
@@ -782,3 +813,33 @@ def test_fresh_build_ignores_prior_words(vbf, ora, n, m, k, strategy):
     want = np.zeros(nw, np.uint32)
     np.bitwise_or.at(want, (hs >> np.uint64(5)).astype(np.int64), (np.uint32(1) << (hs & np.uint64(31)).astype(np.uint32)))
     assert np.array_equal(got, want)
+
+
+def test_build_workspace_cap_halves_the_chunk(vbf):
+    """a partitioned build whose one-chunk workspace cannot be allocated runs in
+    smaller chunks instead of failing with VBF_ENOMEM.  VBF_WS_MAX_BYTES caps the workspace: 60M
+    keys x k = 10 (6e8 bit indices, ~1.6 GB of workspace in one chunk) under a 0.9 GB cap run in
+    chunks of 2^28 indices -- the same words as the one-chunk build, fresh (into garbage) and ORed
+    into earlier words; a cap below the smallest chunk's workspace is VBF_ENOMEM."""
+    import os
+    n, L, m, k = 60_000_000, 16, 600_000_000, 10
+    keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
+    vbf._lib.call("vbf_gen_fixed_dev", 0x5EED0E71, 0, n, L, _ptr(keys), _stream())
+    want = torch.zeros((m + 31) // 32, dtype=torch.int32, device=DEV)
+    vbf._lib.call("vbf_build_dev_ex", _ptr(keys), None, L, n, 1, m, k, _ptr(want), 2, _stream())
+    torch.cuda.synchronize()
+    os.environ["VBF_WS_MAX_BYTES"] = str(900_000_000)
+    try:
+        fresh = torch.full_like(want, -1)
+        vbf._lib.call("vbf_build_dev_ex", _ptr(keys), None, L, n, 1, m, k, _ptr(fresh), 2 | 0x100, _stream())
+        half = torch.zeros_like(want)
+        vbf._lib.call("vbf_build_dev_ex", _ptr(keys), None, L, n // 2, 1, m, k, _ptr(half), 2, _stream())
+        vbf._lib.call("vbf_build_dev_ex", _ptr(keys[n // 2 * L:]), None, L, n - n // 2, 1, m, k, _ptr(half), 2,
+                      _stream())
+        torch.cuda.synchronize()
+        assert torch.equal(fresh, want) and torch.equal(half, want)
+        os.environ["VBF_WS_MAX_BYTES"] = str(100_000_000)
+        with pytest.raises(vbf.VbfError, match="VBF_WS_MAX_BYTES"):
+            vbf._lib.call("vbf_build_dev_ex", _ptr(keys), None, L, n, 1, m, k, _ptr(half), 2, _stream())
+    finally:
+        os.environ.pop("VBF_WS_MAX_BYTES", None)

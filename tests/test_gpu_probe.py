@@ -31,6 +31,9 @@ CASES = [  # (L or None for var-length, len_prefix, m, k, n)
     (8, 1, 40_000_003, 32, 200_000), (16, 1, 100_000_007, 21, 300_000), (None, 1, 2_500_000_001, 7, 300_000),
     # ... and for keys hashed without the length prefix (pre-encoded integer keys)
     (16, 0, 100_000_007, 14, 300_000), (None, 0, 300_000_007, 23, 300_000), (8, 0, 3_000_000_017, 5, 400_000),
+    # ... at the reference's saturated size m = 2^32 - 1: class 8 (rk_c) with fixed and
+    # class 16 (rk_d) with variable-length keys
+    (8, 0, 4_294_967_295, 6, 300_000), (None, 0, 4_294_967_295, 14, 300_000),
 ]
 
 
@@ -145,3 +148,82 @@ def test_position_table_probe_matches_round3_pipeline(vbf, ora, L, m, k, n):
         lo, hi = int(o_h[sl.start]), int(o_h[sl.stop])
         batch = vbf.pack_offsets(kb[lo:hi], o_h[sl.start:sl.stop + 1] - lo, 1)
     assert np.array_equal(ora.probe(batch, m, k, words.cpu().numpy().view(np.uint32)).astype(np.uint8), res["1"][0][sl])
+
+
+def _probe_both(torch, call, P, keys, offs, stride, n, lp, m, k, words, env):
+    """answers + count of the partitioned probe (strategy 2) under the given environment"""
+    import os
+    old = {kk: os.environ.get(kk) for kk in env}
+    os.environ.update(env)
+    try:
+        o = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        call("vbf_probe_dev_ex", P(keys), P(offs), stride, n, lp, m, k, P(words), P(o), 2, None)
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+        call("vbf_probe_count_dev_ex", P(keys), P(offs), stride, n, lp, m, k, P(words), P(cnt), 2, None)
+        torch.cuda.synchronize()
+        return o.cpu().numpy(), int(cnt.item())
+    finally:
+        for kk, v in old.items():
+            if v is None:
+                os.environ.pop(kk, None)
+            else:
+                os.environ[kk] = v
+
+
+@pytest.mark.parametrize("L,n,chunk_log2", [
+    (32, 1_000_000, None), (16, 700_001, None), (8, 300_000, None), (24, 400_000, None),
+    (32, 1, None), (32, 6_531, None), (32, 6_532, None), (32, 6_533, None), (32, 13_065, None),
+    (32, 10_000_000, "22"),   # 2^22 indices per chunk: 161 tiles = 1 051 652 keys, ten chunks
+])
+def test_round6_probe_on_build_image(vbf, ora, L, n, chunk_log2):
+    """The round-6 probe (vbf_probe_pu.hip: the build's unpadded tile image, padded result bits,
+    posv) at config 5's shape -- m = 2^32 - 1 (the reference's saturated size, bf.rs:230-233),
+    k = 4 -- against the round-3 pipeline (VBF_PROBE_PU=0), the gather probe and the oracle: answers
+    and counts, half the batch positive; single keys, tile edges (6 532 keys per tile), several
+    chunks.  Anchor: contains(), bf.rs:95-105."""
+    import torch
+    from velarixdb_amd._lib import call
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    m, k = 4_294_967_295, 4
+    keys, offs, stride = _keys(torch, L, n, 0x5EED0161)
+    words = torch.zeros((m + 31) // 32, dtype=torch.int32, device="cuda:0")
+    half = max(1, n // 2)
+    call("vbf_build_dev_ex", P(keys), P(offs), stride, half, 1, m, k, P(words), 0, None)
+    env = {"VBF_PROBE_CHUNK_LOG2": chunk_log2} if chunk_log2 else {}
+    pu = _probe_both(torch, call, P, keys, offs, stride, n, 1, m, k, words, env)
+    r3 = _probe_both(torch, call, P, keys, offs, stride, n, 1, m, k, words, {"VBF_PROBE_PU": "0"})
+    g = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    call("vbf_probe_dev_ex", P(keys), P(offs), stride, n, 1, m, k, P(words), P(g), 1, None)
+    torch.cuda.synchronize()
+    assert np.array_equal(pu[0], r3[0]) and np.array_equal(pu[0], g.cpu().numpy())
+    assert pu[1] == r3[1] == int(pu[0].sum())
+    assert pu[0][:half].all()
+    sl = slice(max(0, half - 1000), min(n, half + 30000))
+    batch = vbf.pack_fixed(keys.cpu().numpy().reshape(n, L)[sl], 1)
+    assert np.array_equal(ora.probe(batch, m, k, words.cpu().numpy().view(np.uint32)).astype(np.uint8), pu[0][sl])
+
+
+def test_round6_probe_skewed_runs(vbf, ora):
+    """Heavily repeated keys: every tile's entries fall in a handful of segments, so runs are
+    thousands of entries long -- the segment pass's loop past 4 x 64 groups per batch and the lane
+    that loads its run's next group itself.  Plus a filter with garbage bits set everywhere (mixed
+    answers in every result byte)."""
+    import torch
+    from velarixdb_amd._lib import call
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    m, k, L, n = 4_294_967_295, 4, 32, 2_000_000
+    base, _, _ = _keys(torch, L, 5, 0x5EED0171)
+    idx = torch.arange(n, device="cuda:0") % 5
+    keys = base.view(5, L)[idx].reshape(-1).contiguous()
+    keys.view(n, L)[n // 3:, 0] ^= 0x5A  # a second and third population, 4 of 5 of them unbuilt
+    for words in (torch.zeros((m + 31) // 32, dtype=torch.int32, device="cuda:0"),
+                  torch.randint(-2**31, 2**31 - 1, ((m + 31) // 32,), dtype=torch.int32, device="cuda:0")
+                  & torch.randint(-2**31, 2**31 - 1, ((m + 31) // 32,), dtype=torch.int32, device="cuda:0")):
+        call("vbf_build_dev_ex", P(keys), None, L, n // 3, 1, m, k, P(words), 0, None)
+        pu = _probe_both(torch, call, P, keys, None, L, n, 1, m, k, words, {})
+        r3 = _probe_both(torch, call, P, keys, None, L, n, 1, m, k, words, {"VBF_PROBE_PU": "0"})
+        assert np.array_equal(pu[0], r3[0]) and pu[1] == r3[1] == int(pu[0].sum())
+        assert pu[0][:n // 3].all()
+        uniq, first = np.unique(keys.cpu().numpy().reshape(n, L), axis=0, return_index=True)
+        want = ora.probe(vbf.pack_fixed(uniq, 1), m, k, words.cpu().numpy().view(np.uint32)).astype(np.uint8)
+        assert np.array_equal(want, pu[0][first])

@@ -132,13 +132,18 @@ def test_config5_rank_shape_fresh(vbf, ora):
     assert np.array_equal(w_fresh.cpu().numpy().view(np.uint32), want)
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_config5_full_size_fpr_vs_oracle(vbf, ora):
     """Config 5 at its full size on one GPU (the bench's --config 5 workload): 1B x 32 B keys,
     m = 2^32 - 1, k = 4 ("false-positive rate matched to reference", BASELINE.json configs[4]).
-    The GPU's answers for 10M negatives (bench.py's negative set) equal the oracle's contains
-    (bf.rs:95-105) over the same words key for key, so the FPR is the reference's exact count,
-    and it sits at the rate the saturated sizing gives (fill^k)."""
+    The fresh build -- one partitioned chunk of 4e9 bit indices (kBuildChunkIdx = 2^32) -- equals
+    the 16-thread oracle's words over ALL 1B keys (bf.rs:84-92,230-233; the keys go to the host
+    in slices of 250M, ORed into one word array); the full positive sweep finds every key
+    (contains, bf.rs:95-105, the round-6 probe on the build's image and the round-3 pipeline);
+    and the GPU's answers for 10M negatives (bench.py's negative set) equal the oracle's contains
+    over the same words key for key, so the FPR is the reference's exact count, at the rate the
+    saturated sizing gives (fill^k)."""
+    import os
     from velarixdb_amd.keys import HostBatch
     from velarixdb_amd.workloads import SEED_CFG5, fpr_for_bits_per_key
     N, L = 1_000_000_000, 32
@@ -149,7 +154,29 @@ def test_config5_full_size_fpr_vs_oracle(vbf, ora):
     vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG5, 0, N, L, vp(keys), sp())
     words = torch.randint(-2**31, 2**31 - 1, ((m + 31) // 32,), dtype=torch.int32, device=DEV)
     build(vbf, keys, None, L, N, m, k, 2 | FRESH, words=words)
-    del keys
+    # the full positive sweep (BASELINE configs[4]): every one of the 1B keys hits, on both
+    # partitioned pipelines and the gather probe
+    for strat, env in ((2, None), (2, "0"), (1, None)):
+        if env is not None:
+            os.environ["VBF_PROBE_PU"] = env
+        try:
+            c = torch.zeros(1, dtype=torch.int64, device=DEV)
+            vbf._lib.call("vbf_probe_count_dev_ex", vp(keys), None, L, N, 1, m, k, vp(words), vp(c), strat, sp())
+            assert int(c.item()) == N, (strat, env)
+        finally:
+            os.environ.pop("VBF_PROBE_PU", None)
+    # the words, bit for bit, against the oracle over all 1B keys
+    wh = words.cpu().numpy().view(np.uint32)
+    want = np.zeros_like(wh)
+    S = 250_000_000
+    for lo in range(0, N, S):
+        host = keys[lo * L:(lo + S) * L].cpu().numpy()
+        if lo == 0:  # the device generator is the oracle's (a slice of it)
+            assert np.array_equal(host[:1_000_000 * L], ora.gen_fixed(SEED_CFG5, 0, 1_000_000, L))
+        ora.build_words(HostBatch(host, None, L, S, 1), m, k, words=want, threads=16)
+        del host
+    assert np.array_equal(wh, want)
+    del keys, want
     nn = 10_000_000
     nk = torch.empty(nn * L, dtype=torch.uint8, device=DEV)
     vbf._lib.call("vbf_gen_fixed_dev", SEED_CFG5 ^ 0xFF, N, nn, L, vp(nk), sp())  # bench.py rank 0
@@ -160,7 +187,7 @@ def test_config5_full_size_fpr_vs_oracle(vbf, ora):
     got = out.cpu().numpy()
     host_neg = nk.cpu().numpy()
     assert np.array_equal(host_neg, ora.gen_fixed(SEED_CFG5 ^ 0xFF, N, nn, L))
-    want = ora.probe(HostBatch(host_neg, None, L, nn, 1), m, k, words.cpu().numpy().view(np.uint32), threads=16)
+    want = ora.probe(HostBatch(host_neg, None, L, nn, 1), m, k, wh, threads=16)
     assert np.array_equal(got, want)
     assert fp == int(want.sum())
     assert abs(fp / nn - fill ** k) < 1e-3
@@ -247,11 +274,14 @@ def test_config3_full_size_bit_exact(vbf, ora):
     assert abs(fp / nn - fill ** k) < 5e-4
 
 
-def test_multi_chunk_partitioned_paths(vbf):
+@pytest.mark.timeout(600)
+def test_multi_chunk_partitioned_paths(vbf, ora):
     """More bit indices in one call than one chunk holds (build: kBuildChunkIdx = 2^32, probe:
     kPartChunkIdx = 2^30): both partitioned paths process the batch in chunks.  The chunked
-    build must equal the per-key atomic build bit for bit, and both probe strategies must find
-    every key."""
+    build equals the per-key atomic build bit for bit and the 16-thread oracle over all 440M keys
+    (no longer HIP against HIP only), and both probe strategies find every
+    key."""
+    from velarixdb_amd.keys import HostBatch
     from velarixdb_amd.workloads import SEED_CFG2
     n, L, m, k = 440_000_000, 16, 4_000_000_000, 10  # 4.4e9 indices: 2 build / 5 probe chunks
     keys = torch.empty(n * L, dtype=torch.uint8, device=DEV)
@@ -259,7 +289,12 @@ def test_multi_chunk_partitioned_paths(vbf):
     w_part = build(vbf, keys, None, L, n, m, k, 2)
     w_atom = build(vbf, keys, None, L, n, m, k, 1)
     assert torch.equal(w_part, w_atom)
+    del w_atom
     for strat in (1, 2):
         c = torch.zeros(1, dtype=torch.int64, device=DEV)
         vbf._lib.call("vbf_probe_count_dev_ex", vp(keys), None, L, n, 1, m, k, vp(w_part), vp(c), strat, sp())
         assert int(c.item()) == n, strat
+    host = keys.cpu().numpy()
+    del keys
+    want = ora.build_words(HostBatch(host, None, L, n, 1), m, k, threads=16)
+    assert np.array_equal(w_part.cpu().numpy().view(np.uint32), want)

@@ -208,6 +208,28 @@ def test_handle_semantics_host():
     assert bf.no_of_elements == 7 and bf.serialize()[4:8] == (7).to_bytes(4, "little")
 
 
+def test_pristine_host_filter_holds_no_host_words():
+    """BloomFilter::new on the host (bf.rs:62-81) allocates no bit array until its
+    first use -- the compaction filter (sized.rs:192-193) goes new -> migrate to a GPU without
+    touching host memory.  Reading a never-written filter gives zeros; the first set allocates
+    the words; clear keeps them; a contains on a fresh filter answers false (m > 0, k > 0)."""
+    from velarixdb_amd import HOST, BloomFilter
+    bf = BloomFilter(1e-4, 2_000_000, device=HOST)  # m = 38.3M bits: 4.8 MB of words
+    assert bf.host_bytes == 0
+    assert bf.no_of_hash_func == 19 and bf.num_bits() == 38_340_233
+    c = bf.clone()  # shares the (still unallocated) bits
+    assert c.host_bytes == 0
+    w = bf.words()
+    assert w.shape == (bf.num_words(),) and not w.any() and bf.host_bytes == 0
+    fresh = bf.clear()
+    assert bf.host_bytes == 0 and fresh.host_bytes == 0
+    assert not bf.contains(b"never set")
+    assert bf.host_bytes == bf.num_words() * 4  # the probe needs the words: allocated, zero
+    g = BloomFilter(1e-4, 1000, device=HOST)
+    g.set(b"key")
+    assert g.host_bytes == g.num_words() * 4 and g.contains(b"key") and c.host_bytes == bf.host_bytes
+
+
 def test_host_filter_rejects_device_entry_points():
     from velarixdb_amd import HOST, BloomFilter
     from velarixdb_amd._lib import VBF_EINVAL, lib

@@ -11,6 +11,9 @@
 // into a checksum.  Run lengths per (tile, segment): mean M, uniform +-M/2.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/rdflat tools/rdflat.hip
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <vector>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -130,7 +133,16 @@ static float run(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles, uint3
     return ms / 5;
 }
 
-int main() {
+// usage: rdflat [formats]   formats: comma-separated of 0 (g20, the shipped group image), 1 (g16),
+// 2 (raw20), 3 (g20loc: slot-table locate), 4 (g20nt: non-temporal group loads); default "0"
+// (profiles/r05/rdflat_nt.txt ran "0,4", profiles/r04/rdflat*.log "0,1,2" and "0,3")
+int main(int argc, char** argv) {
+    std::vector<int> fmts;
+    for (const char* p = argc > 1 ? argv[1] : "0"; *p;) {
+        fmts.push_back((int)strtol(p, (char**)&p, 10));
+        if (*p == ',') ++p;
+        else if (*p) return 2;
+    }
     struct Cfg { const char* name; uint32_t ntiles, nseg, mean; };
     // k = 10: 100M keys / 3072 per tile, m = 1e9; k = 19: 100M / 1536, m = 1.9e9; and 19 with a
     // 3072-key tile (one k_tile_pack workgroup per CU)
@@ -146,7 +158,7 @@ int main() {
         hipLaunchKernelGGL(k_gen, dim3((c.ntiles + 255) / 256), dim3(256), 0, 0, bnd, c.ntiles, c.nseg, c.mean, used);
         uint32_t cap = 0;
         (void)hipMemcpy(&cap, used, 4, hipMemcpyDeviceToHost);
-        for (int fmt : {0}) {
+        for (int fmt : fmts) {
             const uint32_t tile_bytes = fmt != 1 ? ((cap + 7) / 8 * 20 + 16 + 15) & ~15u : ((cap + 5) / 6 * 16 + 16);
             const uint64_t bytes = (uint64_t)c.ntiles * tile_bytes + 4096;
             uint8_t* img;

@@ -56,6 +56,7 @@ SIGNATURES = {
     "vbf_probe_count_dev_ex": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _u32, _vp, _vp, _int, _vp]),
     "vbf_hashes_dev": (_int, [_vp, _vp, _u64, _u64, _int, _u32, _vp, _vp]),
     "vbf_or_words_dev": (_int, [_vp, _vp, _u64, _vp]),
+    "vbf_or_fold_dev": (_int, [_vp, _vp, _u64, _u32, _u64, _vp]),
     "vbf_popcount_dev": (_int, [_vp, _u64, _vp, _vp]),
     "vbf_gen_fixed_dev": (_int, [_u64, _u64, _u64, _u32, _vp, _vp]),
     "vbf_gen_var_dev": (_int, [_u64, _u64, _u64, _vp, _vp, _vp]),
@@ -85,6 +86,7 @@ SIGNATURES = {
     "vbf_filter_num_hash_functions": (_u32, [_vp]),
     "vbf_filter_false_positive_rate": (_dbl, [_vp]),
     "vbf_filter_device": (_int, [_vp]),
+    "vbf_filter_host_bytes": (_u64, [_vp]),
     "vbf_filter_words_dev": (_vp, [_vp]),
     "vbf_filter_words_dev_read": (_vp, [_vp]),
     "vbf_filter_set_sst_entries": (_int, [_vp, _u64]),

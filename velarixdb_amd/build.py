@@ -1,11 +1,12 @@
 """Build libvbf.so in-tree for gfx950 (explicit hipcc; the .so travels with the repo snapshot)."""
 import os
+import re
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["vbf_kernels.hip", "vbf_partition.hip", "vbf_partition_rk_a.hip", "vbf_partition_rk_b.hip", "vbf_partition_rk_c.hip", "vbf_partition_rk_d.hip", "vbf_partition_sat.hip", "vbf_partition_k1_a.hip", "vbf_partition_k1_b.hip", "vbf_partition_k1_c.hip", "vbf_probe_part.hip", "vbf_probe_part_rk_a.hip", "vbf_probe_part_rk_b.hip", "vbf_probe_part_rk_c.hip", "vbf_probe_part_rk_d.hip", "vbf_sst.hip", "vbf_multi.hip", "vbf_multi_part.hip", "vbf_compact.hip", "vbf_api.hip"]
+SOURCES = ["vbf_kernels.hip", "vbf_partition.hip", "vbf_partition_rk_a.hip", "vbf_partition_rk_b.hip", "vbf_partition_rk_c.hip", "vbf_partition_rk_d.hip", "vbf_partition_sat.hip", "vbf_partition_k1_a.hip", "vbf_partition_k1_b.hip", "vbf_partition_k1_c.hip", "vbf_probe_part.hip", "vbf_probe_part_rk_a.hip", "vbf_probe_part_rk_b.hip", "vbf_probe_part_rk_c.hip", "vbf_probe_part_rk_d.hip", "vbf_probe_pu.hip", "vbf_sst.hip", "vbf_multi.hip", "vbf_multi_part.hip", "vbf_compact.hip", "vbf_api.hip"]
 OUT = os.path.join(HERE, "libvbf.so")
 ARCH = os.environ.get("VBF_OFFLOAD_ARCH", "gfx950")
 
@@ -15,6 +16,26 @@ def _hipcc():
         if c and (os.path.sep not in c or os.path.exists(c)):
             return c
     raise RuntimeError("hipcc not found")
+
+
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _deps(path, seen=None):
+    """The file and every quoted include it reaches in csrc/ or include/."""
+    seen = set() if seen is None else seen
+    if path in seen or not os.path.exists(path):
+        return seen
+    seen.add(path)
+    with open(path, errors="replace") as f:
+        text = f.read()
+    for name in _INC.findall(text):
+        for d in (os.path.dirname(path), CSRC, os.path.join(HERE, "..", "include")):
+            cand = os.path.normpath(os.path.join(d, name))
+            if os.path.exists(cand):
+                _deps(cand, seen)
+                break
+    return seen
 
 
 def needs_build():
@@ -37,15 +58,14 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     os.makedirs(objdir, exist_ok=True)
     flags = ["--offload-arch=" + ARCH, "-O3", "-std=c++20", "-fPIC", "-Wall"] + ["-D" + d for d in defines]
     procs, objs = [], []
-    # an object is current when newer than its source, every header and this script
-    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hpp")] + [
-        os.path.join(HERE, "..", "include", "vbf.h"), __file__]
-    t_hdr = max(os.path.getmtime(h) for h in hdrs if os.path.exists(h))
+    # an object is current when newer than its source and the headers it includes (transitively,
+    # csrc/ and include/); build(force=True) after changing the flags
     for s in SOURCES:
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
         objs.append(obj)
         src = os.path.join(CSRC, s)
-        if (not force and os.path.exists(obj) and os.path.getmtime(obj) > max(t_hdr, os.path.getmtime(src))):
+        t_dep = max(os.path.getmtime(d) for d in _deps(src))
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > t_dep:
             continue
         cmd = [_hipcc()] + flags + ["-c", src, "-o", obj]
         if verbose:

@@ -171,10 +171,19 @@ struct Workspace {
 std::mutex g_ws_mu;
 std::vector<Workspace> g_ws;
 
+// VBF_WS_MAX_BYTES (read per call): the largest single workspace the library may allocate -- for a
+// caller sharing the GPU; a build whose default chunk needs more runs in smaller chunks (do_build)
+uint64_t ws_max_bytes() {
+    const char* e = getenv("VBF_WS_MAX_BYTES");
+    return e ? strtoull(e, nullptr, 10) : ~0ull;
+}
+
 int get_workspace(hipStream_t s, uint64_t bytes, void** out, int slot = kWsBuild) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     bytes = std::max<uint64_t>(bytes, 256);
+    if (bytes > ws_max_bytes())
+        return fail(VBF_ENOMEM, "workspace of %llu bytes above VBF_WS_MAX_BYTES", (unsigned long long)bytes);
     std::lock_guard<std::mutex> lk(g_ws_mu);
     for (auto& w : g_ws) {
         if (w.device == dev && w.stream == s && w.slot == slot) {
@@ -232,14 +241,22 @@ int do_build(const vbf::KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words, i
         HIP_TRY(vbf::launch_build(kb, m, k, words, s));
         return VBF_OK;
     }
-    const bool fused = fresh && !atomic_merge && vbf::partition_fresh_ok(kb.n, m, k);
+    // The workspace holds one chunk of bit indices (kBuildChunkIdx = 2^32: ~10.7 GB).  When it
+    // cannot be allocated (other streams' workspaces, the caller's own memory), the chunk is halved
+    // down to 2^28 indices -- more segment passes, the same words.
+    uint64_t chunk = vbf::build_chunk_default(), need = 0;
+    void* ws = nullptr;
+    for (;;) {
+        need = vbf::partition_workspace_bytes(kb.n, m, k, chunk);
+        const int rc = get_workspace(s, need, &ws);
+        if (rc == VBF_OK) break;
+        if (rc != VBF_ENOMEM || chunk <= (1ull << 28)) return rc;
+        chunk /= 2;
+    }
+    const bool fused = fresh && !atomic_merge && vbf::partition_fresh_ok(kb.n, m, k, chunk);
     if (fresh && !fused)
         if (int rc = zero()) return rc;
-    const uint64_t need = vbf::partition_workspace_bytes(kb.n, m, k);
-    void* ws = nullptr;
-    int rc = get_workspace(s, need, &ws);
-    if (rc) return rc;
-    HIP_TRY(vbf::launch_build_partitioned(kb, m, k, words, ws, need, atomic_merge, s, fused));
+    HIP_TRY(vbf::launch_build_partitioned(kb, m, k, words, ws, need, atomic_merge, s, fused, chunk));
     return VBF_OK;
 }
 
@@ -408,6 +425,7 @@ struct Staging {
     uint32_t* d_words = nullptr;  // scratch filter for the one-shot host API
     uint64_t words_cap = 0;
     uint8_t* h_xfer[2] = {nullptr, nullptr};  // pinned bounce buffers for large filter copies
+    hipEvent_t first = nullptr;  // a fresh filter's first chunk built: the other chunks OR after it
 
     int init(int dev) {
         if (device == dev) return VBF_OK;
@@ -416,6 +434,7 @@ struct Staging {
             HIP_TRY(hipStreamCreateWithFlags(&stream[b], hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&done[b], hipEventDisableTiming));
         }
+        HIP_TRY(hipEventCreateWithFlags(&first, hipEventDisableTiming));
         return VBF_OK;
     }
     template <class T>
@@ -602,6 +621,10 @@ struct Storage {
     uint32_t m = 0;
     uint64_t nwords = 0;
     uint32_t* d_words = nullptr;
+    // Host-resident bits.  Allocated on first use (host_words): a filter that is created on the
+    // host and moved to a GPU before any set -- the compaction filter, bf.rs:62-81 then
+    // build_filter_from_entries -- never zero-fills m/8 bytes of host memory.
+    // Empty while pristine and never touched = all zero.
     std::vector<uint32_t> h_words;
     // The last asynchronous operation on d_words (a _dev call on the caller's stream): later
     // calls on other streams wait for it on the device, host-side calls wait for it on the host,
@@ -657,6 +680,12 @@ struct Storage {
         if (last) (void)hipEventDestroy(last);
     }
 };
+
+// Caller holds s.mu, host-resident storage: the words, allocated (zeroed) on first use.
+uint32_t* host_words(Storage& s) {
+    if (s.h_words.size() != s.nwords) s.h_words.assign(s.nwords, 0u);
+    return s.h_words.data();
+}
 
 // Caller holds s.mu: true when every queued asynchronous job has run.  Jobs queued by the parent
 // of a forked child never run in the child (the worker thread stayed in the parent): the child
@@ -844,14 +873,16 @@ int new_storage(int device, uint32_t m, std::shared_ptr<Storage>* out) {
     s->m = m;
     s->nwords = ((uint64_t)m + 31) / 32;
     if (device == VBF_DEVICE_HOST) {
-        s->h_words.assign(s->nwords, 0u);
+        // BitVec::from_elem(m, false) (bf.rs:71): allocated on first use (host_words)
     } else if (s->nwords) {
         hipStream_t st;
         int rc = filter_stream(device, &st);
         if (rc) return rc;
         HIP_TRY(hipMalloc((void**)&s->d_words, s->nwords * 4));
+        // zeroed on the filter's stream, not waited for: every later use of the words is ordered
+        // after the filter's last event (storage_wait / storage_sync)
         HIP_TRY(hipMemsetAsync(s->d_words, 0, s->nwords * 4, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        if ((rc = storage_mark(*s, st))) return rc;
     }
     *out = std::move(s);
     return VBF_OK;
@@ -1016,10 +1047,23 @@ int device_set_host(Storage& s, uint32_t k, const uint8_t* keys, const uint64_t*
     if (rc) return rc;
     if ((rc = storage_sync(s))) return rc;  // earlier _dev work on this filter, any stream
     s.mirror_ok = false;
+    // A pristine filter (new or cleared, never written: the compaction filter, sized.rs:192-193)
+    // takes its first chunk as BloomFilter::new fused with the build (VBF_BUILD_FRESH: the segment
+    // pass writes its words without reading them, where one chunk and one workgroup per segment
+    // allow), as the benchmark's step does; the other chunks wait for it on the device, then OR
+    // in with word atomics as before.
+    const bool fresh = s.pristine;
     s.pristine = false;
     rc = pipeline_host_keys(
         *st, keys, offsets, stride, n, lp, false,
-        [&](const vbf::KeyBatch& kb, uint64_t, int, hipStream_t hs) -> int {
+        [&](const vbf::KeyBatch& kb, uint64_t lo, int, hipStream_t hs) -> int {
+            if (fresh && lo == 0) {
+                int r = do_build(kb, s.m, k, s.d_words, VBF_BUILD_AUTO | VBF_BUILD_FRESH, false, hs);
+                if (r) return r;
+                HIP_TRY(hipEventRecord(st->first, hs));
+                return VBF_OK;
+            }
+            if (fresh) HIP_TRY(hipStreamWaitEvent(hs, st->first, 0));
             return do_build(kb, s.m, k, s.d_words, VBF_BUILD_AUTO, true, hs);
         },
         [](int, uint64_t, uint64_t) { return VBF_OK; });
@@ -1339,6 +1383,25 @@ int vbf_or_words_dev(uint32_t* dst, const uint32_t* src, uint64_t nwords, void* 
     return ok();
 }
 
+extern "C++" {
+namespace vbf {  // vbf_kernels.hip
+hipError_t launch_or_fold(uint32_t* dst, const uint32_t* src, uint64_t nwords, uint32_t parts, uint64_t pstride,
+                          hipStream_t s);
+}
+}
+
+int vbf_or_fold_dev(uint32_t* dst, const uint32_t* src, uint64_t nwords, uint32_t nparts, uint64_t part_stride,
+                    void* stream) {
+    FORK_GUARD();
+    if (nwords && nparts && (!dst || !src)) return fail(VBF_EINVAL, "NULL words");
+    if (nparts > 1 && part_stride < nwords) return fail(VBF_EINVAL, "parts overlap (stride %llu < %llu words)",
+                                                        (unsigned long long)part_stride, (unsigned long long)nwords);
+    const hipError_t e = vbf::launch_or_fold(dst, src, nwords, nparts, part_stride, (hipStream_t)stream);
+    if (e == hipErrorInvalidValue) return fail(VBF_EINVAL, "vbf_or_fold_dev needs 16-byte aligned words and a stride of whole 4-word units");
+    HIP_TRY(e);
+    return ok();
+}
+
 int vbf_popcount_dev(const uint32_t* words, uint64_t nwords, unsigned long long* count_dev, void* stream) {
     FORK_GUARD();
     if (!count_dev || (nwords && !words)) return fail(VBF_EINVAL, "NULL argument");
@@ -1540,10 +1603,20 @@ int vbf_filter_device(const vbf_filter* f) {
     std::lock_guard<std::mutex> lk(f->bits->mu);
     return f->bits->device;
 }
+uint64_t vbf_filter_host_bytes(const vbf_filter* f) {
+    if (!f) return 0;
+    Storage& s = *f->bits;
+    std::lock_guard<std::mutex> lk(s.mu);
+    return (uint64_t)s.h_words.size() * 4 + (s.mirror ? s.nwords * 4 : 0);
+}
+
 uint32_t* vbf_filter_words_dev(const vbf_filter* f) {
     if (!f) return nullptr;
     Storage& s = *f->bits;
     std::lock_guard<std::mutex> lk(s.mu);
+    // the caller's kernels are not ordered after the filter's last event (e.g. the asynchronous
+    // zeroing of a new filter's words): wait for it here
+    if (!hip_forked() && storage_sync(s) != VBF_OK) return nullptr;
     if (s.d_words) {
         // the caller may write through the pointer: the bits are no longer known to be zero, and
         // the host mirror is bypassed until the write is declared (vbf_filter_stream_record)
@@ -1558,6 +1631,7 @@ const uint32_t* vbf_filter_words_dev_read(const vbf_filter* f) {
     if (!f) return nullptr;
     Storage& s = *f->bits;
     std::lock_guard<std::mutex> lk(s.mu);
+    if (!hip_forked() && storage_sync(s) != VBF_OK) return nullptr;  // as vbf_filter_words_dev
     return s.d_words;  // read-only use: the mirror and `pristine` stay trusted
 }
 
@@ -1621,7 +1695,7 @@ int vbf_filter_set_host(vbf_filter* f, const uint8_t* keys, const uint64_t* offs
     if (n && f->k) {
         if (s.host()) {
             s.pristine = false;
-            host_set(s.h_words.data(), s.m, f->k, keys, offsets, stride, n, len_prefix != 0);
+            host_set(host_words(s), s.m, f->k, keys, offsets, stride, n, len_prefix != 0);
         } else {
             DEVICE_SCOPE(s.device);
             if ((rc = device_set_host(s, f->k, keys, offsets, stride, n, len_prefix))) return rc;
@@ -1670,11 +1744,14 @@ int vbf_filter_set_host_async(vbf_filter* f, const uint8_t* keys, const uint64_t
         if ((rc = storage_drain(s, lk))) return rc;
         if (n && f->k) {
             s.pristine = false;
-            host_set(s.h_words.data(), s.m, f->k, j->keys, j->offsets, stride, n, len_prefix != 0);
+            host_set(host_words(s), s.m, f->k, j->keys, j->offsets, stride, n, len_prefix != 0);
         }
         lk.unlock();
         if (release) release(release_ctx);
     } else {
+        // a forked child: a device-resident filter's set never runs here (HIP is the parent's), so
+        // fail before anything is queued or counted -- no job, no worker thread, no n += N
+        if (hip_forked()) return fail_forked();
         if (s.jobs_pid != getpid() && s.jobs_done != s.jobs_queued) {
             // forked while the parent had sets queued on this filter: they never run here.  Report
             // that now (as every other call does) instead of overwriting jobs_pid, which would make
@@ -1795,7 +1872,7 @@ int vbf_filter_contains_host(const vbf_filter* f, const uint8_t* keys, const uin
     std::unique_lock<std::mutex> lk(s.mu);
     if ((rc = storage_drain(s, lk))) return rc;
     if (s.host()) {
-        host_contains(s.h_words.data(), s.m, f->k, keys, offsets, stride, n, len_prefix != 0, out);
+        host_contains(host_words(s), s.m, f->k, keys, offsets, stride, n, len_prefix != 0, out);
         return ok();
     }
     DEVICE_SCOPE(s.device);
@@ -1857,7 +1934,8 @@ int vbf_filter_clear(vbf_filter* f, vbf_filter** out) {
 static int words_to_host_locked(Storage& s, uint32_t* out) {
     if (!s.nwords) return VBF_OK;
     if (s.host()) {
-        std::memcpy(out, s.h_words.data(), s.nwords * 4);
+        if (s.h_words.empty()) std::memset(out, 0, s.nwords * 4);  // never written: all zero
+        else std::memcpy(out, s.h_words.data(), s.nwords * 4);
         return VBF_OK;
     }
     DEVICE_SCOPE(s.device);
@@ -1890,7 +1968,7 @@ static int words_from_host_locked(Storage& s, const uint32_t* in) {
     if (!s.nwords) return VBF_OK;
     s.pristine = false;
     if (s.host()) {
-        std::memcpy(s.h_words.data(), in, s.nwords * 4);
+        std::memcpy(host_words(s), in, s.nwords * 4);
         return VBF_OK;
     }
     DEVICE_SCOPE(s.device);
@@ -1937,18 +2015,19 @@ int vbf_filter_migrate(vbf_filter* f, int device) {
     const bool zeros = s.pristine;  // nothing to copy: the target gets zeroed words
     if (s.host()) {
         w.swap(s.h_words);
+        if (!zeros && w.size() != s.nwords) w.assign(s.nwords, 0u);  // written words are allocated
     } else {
         DEVICE_SCOPE(s.device);
         if ((rc = storage_sync(s))) return rc;
-        if (!zeros || device == VBF_DEVICE_HOST) w.resize(s.nwords);
+        if (!zeros) w.resize(s.nwords);  // to the host, a pristine filter stays unallocated
         if (s.nwords && !zeros) HIP_TRY(hipMemcpy(w.data(), s.d_words, s.nwords * 4, hipMemcpyDeviceToHost));
     }
     uint32_t* nd = nullptr;
     if (device != VBF_DEVICE_HOST && s.nwords) {
         DEVICE_SCOPE(device);
         hipError_t e = hipMalloc((void**)&nd, s.nwords * 4);
-        if (e == hipSuccess) e = zeros ? hipMemset(nd, 0, s.nwords * 4)
-                                       : hipMemcpy(nd, w.data(), s.nwords * 4, hipMemcpyHostToDevice);
+        // a pristine filter's words are zeroed asynchronously below (no copy, no host wait)
+        if (e == hipSuccess && !zeros) e = hipMemcpy(nd, w.data(), s.nwords * 4, hipMemcpyHostToDevice);
         if (e != hipSuccess) {  // the filter stays where it was, bits intact
             (void)hipGetLastError();
             if (nd) (void)hipFree(nd);
@@ -1969,6 +2048,13 @@ int vbf_filter_migrate(vbf_filter* f, int device) {
     s.d_words = nd;
     if (device == VBF_DEVICE_HOST) s.h_words.swap(w);
     s.device = device;
+    if (nd && zeros) {  // on the filter's stream; every later use waits for the filter's last event
+        DEVICE_SCOPE(device);
+        hipStream_t fs;
+        if ((rc = filter_stream(device, &fs))) return rc;
+        HIP_TRY(hipMemsetAsync(nd, 0, s.nwords * 4, fs));
+        if ((rc = storage_mark(s, fs))) return rc;
+    }
     return ok();
 }
 

@@ -244,6 +244,42 @@ hipError_t launch_or_words(uint32_t* dst, const uint32_t* src, uint64_t nwords, 
     return hipGetLastError();
 }
 
+// dst = src[0] | src[1] | ... | src[parts - 1], the parts `pstride` words apart: the fold of the
+// multi-GPU OR all-reduce (dist.or_allreduce_) in one pass -- every part read once, dst written
+// once -- where parts - 1 k_or_words launches re-read and re-write the accumulator each time.
+__global__ __launch_bounds__(kBlock) void k_or_fold(uint32_t* dst, const uint32_t* src, uint64_t nw, uint32_t parts,
+                                                    uint64_t pstride) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock * 4;
+    for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4; i < nw; i += stride) {
+        if (i + 4 <= nw) {
+            uint4 d = *reinterpret_cast<const uint4*>(src + i);
+            for (uint32_t p = 1; p < parts; ++p) {
+                const uint4 v = *reinterpret_cast<const uint4*>(src + (uint64_t)p * pstride + i);
+                d.x |= v.x; d.y |= v.y; d.z |= v.z; d.w |= v.w;
+            }
+            *reinterpret_cast<uint4*>(dst + i) = d;
+        } else {
+            for (uint64_t t = i; t < nw; ++t) {
+                uint32_t d = src[t];
+                for (uint32_t p = 1; p < parts; ++p) d |= src[(uint64_t)p * pstride + t];
+                dst[t] = d;
+            }
+        }
+    }
+}
+
+hipError_t launch_or_fold(uint32_t* dst, const uint32_t* src, uint64_t nwords, uint32_t parts, uint64_t pstride,
+                          hipStream_t s) {
+    if (nwords == 0 || parts == 0) return hipSuccess;
+    uint64_t blocks = (nwords / 4 + kBlock - 1) / kBlock;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    const bool al = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0 && pstride % 4 == 0;
+    if (!al) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_or_fold, dim3((unsigned)blocks), dim3(kBlock), 0, s, dst, src, nwords, parts, pstride);
+    return hipGetLastError();
+}
+
 // ---- popcount of a filter (fill ratio reporting) ----
 __global__ __launch_bounds__(kBlock) void k_popcount(const uint32_t* w, uint64_t nw,
                                                       unsigned long long* out) {

@@ -43,7 +43,11 @@ void phase_end(int phase, hipStream_t s);
 constexpr uint64_t kPartChunkIdx = 1ull << 30;
 constexpr uint64_t kBuildChunkIdx = 1ull << 32;
 bool partition_supported(uint32_t m, uint32_t k);
-uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
+// chunk_idx: bit indices per build chunk (0: kBuildChunkIdx or VBF_BUILD_CHUNK_LOG2); the C ABI
+// halves it when the workspace for the default chunk cannot be allocated (2^32
+// indices take ~10.7 GB)
+uint64_t build_chunk_default();
+uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k, uint64_t chunk_idx = 0);
 // Partitioned probe (vbf_partition.hip): out (answer bytes) or count (hits), one of them.
 bool probe_partition_supported(uint32_t m, uint32_t k);
 uint64_t probe_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
@@ -54,9 +58,9 @@ uint64_t probe_count_partials(uint64_t n, uint32_t m, uint32_t k);
 // reading it (callers zero the words themselves where that pass cannot own every segment).
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
                                     void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s,
-                                    bool fresh = false);
+                                    bool fresh = false, uint64_t chunk_idx = 0);
 // Whether a fresh build of n keys can skip the zero fill (one chunk, one workgroup per segment).
-bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k);
+bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k, uint64_t chunk_idx = 0);
 hipError_t launch_probe(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words,
                         uint8_t* out, hipStream_t s);
 // Count: `partial` holds count_partials(n) u32 of scratch; the hits are added to *count.

@@ -465,7 +465,7 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
 // class kernels).  group_sb != 0: the position-table pack of the probes (vbf_multi_part.hip:
 // segments of 2^17 bytes of 8 interleaved filters; vbf_probe_part.hip: 2^20 filter bits) -- the
 // 512-thread shape, keys in key order, runs padded to whole groups.
-static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = true, int group_sb = 0) {
+static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = true, int group_sb = 0, bool pu = false) {
     PartPlan pl{};
     const bool group = group_sb != 0;
     const int sb = group ? group_sb : kSegBits;
@@ -512,6 +512,12 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     static const int k14env = [] { const char* e = getenv("VBF_K1_4"); return e ? atoi(e) : 0; }();
     static const int satenv = [] { const char* e = getenv("VBF_SAT"); return e ? atoi(e) : 1; }();
     if (k14env == 1 && satenv != 0 && k == 4 && fixed && lp && m == 0xFFFFFFFFu && !group && pl.c16) pl.k1v = 1;
+    // the round-6 probe pack (K1 with POS = 2, vbf_probe_pu.hip): one u32 counter per segment (the
+    // run's place and padded place in its two halves), the 1 024-thread shape
+    if (pu) {
+        pl.c16 = 0;
+        pl.k1v = 0;
+    }
     const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : k), fixed, (int)pl.k1v);
     const uint32_t rmax = (uint32_t)(ck || pl.kc ? sh.rounds : rounds_max((int)k));
     const uint32_t kpr = (uint32_t)sh.bs / (uint32_t)(ck ? sh.spl : 1);  // keys per round
@@ -597,19 +603,21 @@ static uint64_t build_chunk_idx() {
     return v;
 }
 
-static uint64_t chunk_keys_for(const PartPlan& pl, uint64_t n) {
-    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, build_chunk_idx() / pl.C);
+uint64_t build_chunk_default() { return build_chunk_idx(); }
+
+static uint64_t chunk_keys_for(const PartPlan& pl, uint64_t n, uint64_t chunk_idx = 0) {
+    const uint64_t tiles_per_chunk = std::max<uint64_t>(1, (chunk_idx ? chunk_idx : build_chunk_idx()) / pl.C);
     return std::min<uint64_t>(n, tiles_per_chunk * pl.KT);
 }
 
 // Bytes of workspace one launch_build_partitioned call needs for n keys.
-uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
+uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k, uint64_t chunk_idx) {
     if (!partition_supported(m, k)) return 0;
     uint64_t need = 0;
     for (bool fixed : {true, false})  // the largest of the layouts' plans
         for (bool lp : {true, false}) {
             const PartPlan pl = make_plan(m, k, fixed, lp);
-            const uint64_t ntiles = (chunk_keys_for(pl, n) + pl.KT - 1) / pl.KT;
+            const uint64_t ntiles = (chunk_keys_for(pl, n, chunk_idx) + pl.KT - 1) / pl.KT;
             // tiles, then ends[ntiles][nsegS] and endsT[nsegS][ntiles rounded up to 8] (16-byte aligned)
             need = std::max<uint64_t>(need,
                                       ntiles * (uint64_t)pl.tile_words * 4 + (ntiles + 8) * (uint64_t)pl.nsegS * 4 + 512);
@@ -617,12 +625,12 @@ uint64_t partition_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     return need;
 }
 
-bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k) {
+bool partition_fresh_ok(uint64_t n, uint32_t m, uint32_t k, uint64_t chunk_idx) {
     if (!partition_supported(m, k) || n == 0) return false;
     for (bool fixed : {true, false})
         for (bool lp : {true, false}) {
             const PartPlan pl = make_plan(m, k, fixed, lp);
-            const uint64_t ck = chunk_keys_for(pl, n);
+            const uint64_t ck = chunk_keys_for(pl, n, chunk_idx);
             const uint64_t ntiles = (ck + pl.KT - 1) / pl.KT;
             const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)ntiles, (512 + pl.nseg - 1) / pl.nseg));
             if (ck < n || G > 1) return false;
@@ -646,6 +654,13 @@ bool group_pack_supported(uint64_t m, uint32_t k, int sb) {
 }
 
 PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed, int sb) { return make_plan(m, k, fixed, true, sb); }
+
+PartPlan make_probe_pu_plan(uint32_t m, uint32_t k, bool fixed, bool lp) {
+    PartPlan pl = make_plan(m, k, fixed, lp, 0, true);
+    pl.len_order = 0;  // posv maps lane slots to keys in key order
+    pl.stage_keys = 0;
+    return pl;
+}
 
 uint32_t group_pack_slots(uint32_t k) {
     const K1Shape sh = k1_shape((int)k, true, 1);
@@ -689,14 +704,15 @@ hipError_t launch_tile_pack_main(int fmt, bool lp, const DevKeys& dk, const Part
 }
 
 hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, uint32_t* words,
-                                    void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s, bool fresh) {
+                                    void* ws, uint64_t ws_bytes, bool atomic_merge, hipStream_t s, bool fresh,
+                                    uint64_t chunk_idx) {
     if (kb.n == 0 || k == 0) return hipSuccess;
     if (!partition_supported(m, k)) return hipErrorInvalidValue;
     // every chunk keeps the batch's alignment (chunks are whole tiles of keys), so one layout
     PartPlan pl = make_plan(m, k, pick_fmt(kb.keys, kb.offsets, kb.stride) > 0, kb.len_prefix);
-    const uint64_t chunk_keys = chunk_keys_for(pl, kb.n);
+    const uint64_t chunk_keys = chunk_keys_for(pl, kb.n, chunk_idx);
     const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
-    if (ws_bytes < partition_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;
+    if (ws_bytes < partition_workspace_bytes(kb.n, m, k, chunk_idx)) return hipErrorInvalidValue;
     uint32_t* tiles = reinterpret_cast<uint32_t*>(ws);
     uint16_t* ends = reinterpret_cast<uint16_t*>(
         (reinterpret_cast<uintptr_t>(tiles + max_tiles * pl.tile_words) + 15) & ~(uintptr_t)15);

@@ -68,6 +68,19 @@ __host__ __device__ constexpr K1Shape k1_shape(int k, bool fixed, int v) {
     return K1Shape{kPBlock, build_spl(k, fixed), build_kl(k, fixed), build_rounds_max(k, fixed)};
 }
 
+// Inclusive sum over the lanes of a wave with DPP row shifts and row broadcasts (gfx9 wave64): no
+// ds_bpermute and so no lane-address registers (hipcc hoists and keeps those alive across a kernel,
+// which at 64 VGPRs spills K1's stash).
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); // row_bcast:15 -> rows 1, 3
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 // Exclusive scan of v[0..n) in LDS (n <= PER * blockDim.x, blockDim.x <= kPBlock).  EVEN: scan the
 // counts rounded up to even (the build's even-length runs) in the same pass.  One barrier: after
 // it every wave adds up the totals of the waves before it itself instead of waiting for one wave

@@ -509,6 +509,7 @@ uint64_t probe_workspace_bytes(uint64_t n, uint32_t m, uint32_t k) {
     const uint64_t ntiles = (probe_chunk_keys(pl, n) + pl.KT - 1) / pl.KT;
     uint64_t need = ntiles * ((uint64_t)pl.cap * 4 + pl.cap / 8 + (uint64_t)pl.nseg * 4 + 4) + 1024;
     if (group_pack_supported(m, k, kSegBits)) need = std::max<uint64_t>(need, pp_workspace_bytes(n, m, k));
+    if (probe_pu_enabled(m, k, true, true)) need = std::max<uint64_t>(need, probe_pu_workspace_bytes(n, m, k, true));
     return need;
 }
 
@@ -573,6 +574,8 @@ hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
     const uint64_t chunk_keys = probe_chunk_keys(pl, kb.n);
     const uint64_t max_tiles = (chunk_keys + pl.KT - 1) / pl.KT;
     if (ws_bytes < probe_workspace_bytes(kb.n, m, k)) return hipErrorInvalidValue;
+    if (probe_pu_enabled(m, k, kb.len_prefix, pick_fmt(kb.keys, kb.offsets, kb.stride) > 0))  // round 6: the build's image (vbf_probe_pu.hip)
+        return launch_probe_pu(kb, m, k, words, out, count, ws, ws_bytes, s);
     if (pp_enabled(m, k, kb.len_prefix)) return launch_probe_pp(kb, m, k, words, out, count, ws, s);
     auto align16 = [](uint64_t x) { return (x + 15) & ~15ull; };
     char* base = static_cast<char*>(ws);

@@ -153,18 +153,26 @@ __host__ __device__ constexpr uint32_t group_words(uint32_t entries) { return (e
 // kernels would otherwise take 80-90 and drop to one workgroup per CU.  V = 1: 512 threads, two
 // workgroups per CU at 4 waves per SIMD, 128 VGPRs (k1_shape).
 //
-// SB < kSegBits, POS (the multi-SST group pack, vbf_multi_part.hip): segments of 2^SB positions, and
-// every entry's place in the tile image is also written to posv[tile][stash slot][lane] (u16), so
-// the group output pass finds a key's k results without re-reading the image.
+// POS = 1 (the multi-SST group pack, vbf_multi_part.hip, SB < kSegBits; and the round-4 probe pack):
+// segments of 2^SB positions, every run padded to whole groups in the image, and every entry's
+// place in the tile image is also written to posv[tile][stash slot][lane] (u16), so the group output
+// pass finds a key's k results without re-reading the image.
+// POS = 2 (the round-6 probe pack, vbf_probe_pu.hip): the build's own unpadded image, and beside it
+// the places the entries WOULD have with every run padded to whole groups -- those index the
+// per-entry result bits the segment pass writes (each run owns whole result bytes, so no two
+// workgroups write one byte) -- in posv, and the run ends as u32 pairs (unpadded end | padded
+// end << 16) in endsT.  No padding reserve shrinks the tile (POS = 1 reserves 7 entries per segment
+// of LDS: at m = 2^32 - 1 that is the whole image).
 // SAT: m == 2^32 - 1 (the reference's saturated size), remainders by mod_sat (sip13.hpp).
 template <int FMT, bool LP, int K, bool M31, bool C16 = false, int V = 0, int KC = 0, int SB = kSegBits,
-          bool POS = false, bool SAT = false>
+          int POS = 0, bool SAT = false>
 __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile_pack(DevKeys dk, PartPlan pl,
                                                                                       uint32_t* tiles, uint16_t* ends,
                                                                                       uint16_t* posv) {
     constexpr int BS = V == 1 ? 512 : kPBlock;  // k1_shape(K, FMT > 0, V).bs
     static_assert(V == 0 || K > 0 || KC > 0, "the 512-thread shape is for compiled k and k classes");
     static_assert(KC == 0 || (K == 0 && V == 1 && !C16), "k classes run on the 512-thread shape");
+    static_assert(POS != 2 || (K > 0 || KC > 0), "the probe pack keeps its stash in registers");
     constexpr int KK = K > 0 ? K : KC;  // seed slots per key in the stash (0: the scratch stash)
     extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
     // The per-segment counters first, at LDS address 0 (the kernel has no static LDS, so the
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     // (up to 4 096 segments)
     constexpr int SPER = (V == 1 && !M31) ? 8 : 4;
     auto gd_get = [&](uint32_t sg) -> uint32_t { return (gd[sg >> 1] >> ((sg & 1u) * 16)) & 0xFFFFu; };
-    if constexpr (POS) {
+    if constexpr (POS == 1) {
         // every run padded to whole groups in HBM: gd = groups per segment (u16 pairs), scanned
         // after the counters into each run's first group, then turned into the run's shift
         // dlt(s) = 8 * gstart(s) - start(s) (< 7 * nseg) for the positions written to posv
@@ -350,6 +358,14 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
             const uint32_t d1 = s1 < pl.nseg ? 8 * (g >> 16) - cnt[s1] : 0u;
             gd[w] = d0 | (d1 << 16);
         }
+    } else if constexpr (POS == 2) {
+        // one u32 per segment: count in the low half, its whole result bytes (count rounded up to 8)
+        // in the high half -- one scan makes both the run's start and its padded start, and no half
+        // carries (C + 7 * nseg <= 65535, probe_pu_enabled); each rank atomic adds 1 to both
+        static_assert(!C16, "the probe pack keeps one counter word per segment");
+        for (uint32_t sg = tid; sg < pl.nseg; sg += BS) cnt[sg] |= ((cnt[sg] + 7) & ~7u) << 16;
+        __syncthreads();
+        block_exclusive_scan<false, SPER>(cnt, pl.nseg, wsum);
     } else if constexpr (C16) {
         block_exclusive_scan16<false, SPER>(cnt, pl.nseg, wsum);
     } else {
@@ -357,7 +373,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     }
     // the groups' nibble words start clear (ORed into below); the image held perm / staged keys
     // until the hashing rounds ended
-    for (uint32_t g = tid; g < (POS ? pl.CPg : pl.CP) / 8; g += BS) smem[g * kGroupWords + 4] = 0;
+    for (uint32_t g = tid; g < (POS == 1 ? pl.CPg : pl.CP) / 8; g += BS) smem[g * kGroupWords + 4] = 0;
     __syncthreads();
     if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
         uint32_t acc = 0;
@@ -375,9 +391,12 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             val[q] = (t + q < ns) ? stash[t + q] : kSentinel;
-            pos[q] = val[q] != kSentinel ? seg_rank<C16, SB>(cnt0, val[q]) : 0u;
+            if constexpr (POS == 2)  // place | padded place << 16
+                pos[q] = val[q] != kSentinel ? lds_add_rtn(&cnt0[val[q] >> SB], 0x10001u) : 0u;
+            else
+                pos[q] = val[q] != kSentinel ? seg_rank<C16, SB>(cnt0, val[q]) : 0u;
         }
-        if constexpr (POS) {  // the group pack places every run at its padded place (whole groups)
+        if constexpr (POS == 1) {  // the group pack places every run at its padded place (whole groups)
 #pragma unroll
             for (int q = 0; q < 8; ++q)
                 if (val[q] != kSentinel) pos[q] += gd_get(val[q] >> SB);
@@ -385,27 +404,47 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (val[q] != kSentinel) {
-                const uint32_t g = (pos[q] >> 3) * kGroupWords, e7 = pos[q] & 7;
+                const uint32_t p = POS == 2 ? pos[q] & 0xFFFFu : pos[q];
+                const uint32_t g = (p >> 3) * kGroupWords, e7 = p & 7;
                 lo[g * 2 + e7] = (uint16_t)val[q];
                 atomicOr(&smem[g + 4], ((val[q] >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4));
             }
         }
-        if constexpr (POS) {  // coalesced: for a pair of stash slots the lanes write consecutive u32
+        if constexpr (POS != 0) {  // coalesced: for a pair of stash slots the lanes write consecutive u32
             static_assert(KK > 0, "the group pack runs compiled k");
             uint32_t* pv = reinterpret_cast<uint32_t*>(posv);
+            // POS 1: the place itself (the image is padded); POS 2: the padded place
+            auto pp = [&](int q) -> uint32_t { return val[q] == kSentinel ? 0u : POS == 2 ? pos[q] >> 16 : pos[q]; };
 #pragma unroll
             for (int q = 0; q < 8; q += 2)
                 if (val[q] != kSentinel || val[q + 1] != kSentinel)
-                    pv[((uint64_t)tile * ((kNsMax + 1) / 2) + (t + q) / 2) * BS + tid] =
-                        (val[q] != kSentinel ? pos[q] : 0u) | ((val[q + 1] != kSentinel ? pos[q + 1] : 0u) << 16);
+                    pv[((uint64_t)tile * ((kNsMax + 1) / 2) + (t + q) / 2) * BS + tid] = pp(q) | (pp(q + 1) << 16);
         }
     }
     __syncthreads();
     // cnt[s] = start(s) + count(s) = the end of segment s's run.  The last group's low halves past
     // the tile's end are whatever LDS held: every reader masks entries by the run bounds.
-    const uint32_t total = seg_get<C16>(cnt, pl.nseg - 1);
+    const uint32_t total = seg_get<C16>(cnt, pl.nseg - 1) & (POS == 2 ? 0xFFFFu : 0xFFFFFFFFu);
     uint32_t* out = tiles + (uint64_t)tile * pl.tile_words;
-    if constexpr (POS) {
+    if constexpr (POS == 2) {
+        // the unpadded image, as the build writes it; endsT[s][tile] = end(s) | padded end(s) << 16
+        // (cnt[s] = end | (padded start + count) << 16; the padded start is a multiple of 8)
+        static_assert(SPL == 1, "posv holds one key's seeds per lane");
+        const uint32_t words = group_words(total);
+        for (uint32_t w = tid * 4; w < words; w += BS * 4) {
+            if (w + 4 <= words)
+                image_store(out + w, *reinterpret_cast<const u32x4*>(smem + w));
+            else
+                for (uint32_t x = w; x < words; ++x) out[x] = smem[x];
+        }
+        uint32_t* e32 = reinterpret_cast<uint32_t*>(ends);
+        for (uint32_t sg = tid; sg < pl.nseg; sg += BS) {
+            const uint32_t c = cnt[sg];
+            e32[(uint64_t)sg * pl.ntS + tile] = (c & 0xFFFFu) | ((((c >> 16) + 7) & ~7u) << 16);
+        }
+        return;
+    }
+    if constexpr (POS == 1) {
         // the padded image is already in LDS: copy its whole groups; run ends in padded entries
         // (multiples of 8): end(s) + dlt(s), rounded up to the group
         const uint32_t pwords = group_words((total + gd_get(pl.nseg - 1) + 7) & ~7u);
@@ -462,5 +501,12 @@ hipError_t launch_tile_pack_main_c(int fmt, bool lp, const DevKeys& dk, const Pa
                                    uint32_t* tiles, uint16_t* ends, hipStream_t s);
 hipError_t launch_group_pack(const KeyBatch& kb, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
                              uint32_t* tiles, uint16_t* endsT, uint16_t* posv, int sb, hipStream_t s);
+// The round-6 probe on the build's image (vbf_probe_pu.hip): the build's plan with keys in key order
+// (posv maps a key's seeds to their places), K1 with POS = 2.
+PartPlan make_probe_pu_plan(uint32_t m, uint32_t k, bool fixed, bool lp);
+bool probe_pu_enabled(uint32_t m, uint32_t k, bool lp, bool fixed);
+uint64_t probe_pu_workspace_bytes(uint64_t n, uint32_t m, uint32_t k, bool lp);
+hipError_t launch_probe_pu(const KeyBatch& kb, uint32_t m, uint32_t k, const uint32_t* words, uint8_t* out,
+                           unsigned long long* count, void* ws, uint64_t ws_bytes, hipStream_t s);
 
 }  // namespace vbf

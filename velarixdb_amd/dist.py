@@ -6,8 +6,10 @@
   into a full-width partial array, then the partials are merged with a bitwise-OR
   all-reduce.  RCCL has no OR reduction, so it is composed from data movement plus a local
   OR: all_to_all_single (rank r receives every rank's copy of bit-range r: a reduce-scatter
-  by bit range), the OR of those copies (HIP kernel vbf_or_words_dev on the GPU), then
-  all_gather_into_tensor so every rank holds the full filter for its probe sweep.
+  by bit range), the OR of those copies in one pass (HIP kernel vbf_or_fold_dev: each copy read
+  once, the result written once, into the receive buffer's first slice), then
+  all_gather_into_tensor so every rank holds the full filter for its probe sweep.  The receive
+  buffer is one workspace per (device, size), reused across calls.
 """
 import ctypes
 
@@ -47,26 +49,65 @@ def padded_words(nwords, world, device):
     return torch.zeros(chunk * world, dtype=torch.int32, device=device), chunk
 
 
-def or_allreduce_(buf, chunk, group=None, or_into=or_words_dev):
-    """In place: buf (padded_words layout) becomes the OR of every rank's buf.  The local OR is
-    the HIP kernel; the CPU (gloo) tests of the exchange pattern pass their own `or_into`.
+def or_fold_dev(dst, parts, nparts, chunk):
+    """dst = parts[0:chunk] | parts[chunk:2 chunk] | ... (nparts slices) in one HIP pass
+    (vbf_or_fold_dev); dst may be parts[:chunk] itself.  int32 device tensors."""
+    for t in (dst, parts):
+        if t.device.type != "cuda" or t.dtype != torch.int32 or not t.is_contiguous():
+            raise ValueError("or_fold_dev needs contiguous int32 device tensors")
+    if dst.device != parts.device:
+        raise ValueError("or_fold_dev: dst on %s, parts on %s" % (dst.device, parts.device))
+    if dst.numel() != chunk or parts.numel() < nparts * chunk:
+        raise ValueError("or_fold_dev: dst holds %d words, parts %d (want %d and %d x %d)"
+                         % (dst.numel(), parts.numel(), chunk, nparts, chunk))
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dst.device).cuda_stream)
+    call("vbf_or_fold_dev", ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(parts.data_ptr()), chunk, nparts,
+         chunk, stream)
+
+
+def or_fold_host(dst, parts, nparts, chunk):
+    """The same fold on CPU tensors (the gloo tests of the exchange)."""
+    acc = parts[:chunk].clone()
+    for r in range(1, nparts):
+        acc.bitwise_or_(parts[r * chunk:(r + 1) * chunk])
+    dst.copy_(acc)
+
+
+_recv = {}
+
+
+def _recv_buffer(like):
+    """The all_to_all receive buffer: one per (device, dtype, size), kept for the next call (config 5:
+    a 512 MiB array per rank per step)."""
+    key = (str(like.device), like.dtype, like.numel())
+    t = _recv.get(key)
+    if t is None:
+        t = torch.empty_like(like)
+        _recv[key] = t
+    return t
+
+
+def or_allreduce_(buf, chunk, group=None, fold=None):
+    """In place: buf (padded_words layout) becomes the OR of every rank's buf.  The fold is the HIP
+    kernel for device tensors (or_fold_dev), or `fold` (the CPU gloo tests pass or_fold_host).
 
     Device words under a gloo group (the one-GPU rehearsal of the N > 1 path, where RCCL refuses
     two ranks on one card) move through host tensors for gloo's all_to_all / all_gather, while
-    the fold stays on the GPU: the same HIP OR kernel the RCCL path runs."""
+    the fold stays on the GPU: the same HIP kernel the RCCL path runs."""
     if not dist.is_initialized():
         return buf
     world = dist.get_world_size(group)
     if world == 1:
         return buf
+    if fold is None:
+        fold = or_fold_dev if buf.device.type == "cuda" else or_fold_host
     staged = buf.device.type == "cuda" and dist.get_backend(group) == "gloo"
     src = buf.cpu() if staged else buf
-    recv = torch.empty_like(src)
+    recv = _recv_buffer(src)
     dist.all_to_all_single(recv, src, group=group)
     parts = recv.to(buf.device) if staged else recv
-    acc = parts[:chunk].clone()
-    for r in range(1, world):
-        or_into(acc, parts[r * chunk:(r + 1) * chunk])
+    acc = parts[:chunk]
+    fold(acc, parts, world, chunk)  # into the first slice: every copy read once
     if staged:
         full = torch.empty_like(src)
         dist.all_gather_into_tensor(full, acc.cpu(), group=group)

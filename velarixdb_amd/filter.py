@@ -172,6 +172,11 @@ class BloomFilter:
     def host_resident(self):
         return self.device == VBF_DEVICE_HOST
 
+    @property
+    def host_bytes(self):
+        """Host memory the bits hold (vbf_filter_host_bytes): host words are allocated on first use."""
+        return int(lib.vbf_filter_host_bytes(self._h))
+
     def migrate(self, device):
         """Move the (shared) bit array to GPU `device` or to host memory ("host"), in place."""
         call("vbf_filter_migrate", self._h, _dev(device))
