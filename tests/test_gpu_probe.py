@@ -126,6 +126,7 @@ def test_position_table_probe_matches_round3_pipeline(vbf, ora, L, m, k, n):
     half = n // 2
     call("vbf_build_dev_ex", P(keys), P(offs), stride, half, 1, m, k, P(words), 0, None)
     res = {}
+    os.environ["VBF_PROBE_PU"] = "0"  # the round-6 probe would take k = 10 / 19 at m <= 2^31 first
     for gp in ("1", "0"):
         os.environ["VBF_PROBE_GP"] = gp
         try:
@@ -137,6 +138,7 @@ def test_position_table_probe_matches_round3_pipeline(vbf, ora, L, m, k, n):
             res[gp] = (o.cpu().numpy(), int(cnt.item()))
         finally:
             os.environ.pop("VBF_PROBE_GP", None)
+    os.environ.pop("VBF_PROBE_PU", None)
     assert np.array_equal(res["1"][0], res["0"][0]) and res["1"][1] == res["0"][1] == int(res["1"][0].sum())
     assert res["1"][0][:half].all()
     sl = slice(half - 500, min(n, half + 20000))
@@ -170,21 +172,30 @@ def _probe_both(torch, call, P, keys, offs, stride, n, lp, m, k, words, env):
                 os.environ[kk] = v
 
 
-@pytest.mark.parametrize("L,n,chunk_log2", [
-    (32, 1_000_000, None), (16, 700_001, None), (8, 300_000, None), (24, 400_000, None),
-    (32, 1, None), (32, 6_531, None), (32, 6_532, None), (32, 6_533, None), (32, 13_065, None),
-    (32, 10_000_000, "22"),   # 2^22 indices per chunk: 161 tiles = 1 051 652 keys, ten chunks
+SAT = 4_294_967_295
+
+
+@pytest.mark.parametrize("L,m,k,n,chunk_log2", [
+    (32, SAT, 4, 1_000_000, None), (16, SAT, 4, 700_001, None), (8, SAT, 4, 300_000, None),
+    (24, SAT, 4, 400_000, None), (32, SAT, 4, 1, None), (32, SAT, 4, 6_531, None), (32, SAT, 4, 6_532, None),
+    (32, SAT, 4, 6_533, None), (32, SAT, 4, 13_065, None),
+    (32, SAT, 4, 10_000_000, "22"),   # 2^22 indices per chunk: 160 tiles = 1 045 120 keys, ten chunks
+    # k = 10 / 19 (p = 1e-4: velarixdb's default) at m <= 2^31: the build's 512-thread shape
+    (16, 1_000_000_000, 10, 2_000_000, None), (16, 1_900_000_000, 19, 1_000_000, None),
+    (32, 1 << 31, 19, 600_000, None), (8, 5_000, 10, 300_000, None), (24, 70_000_000, 10, 1_200_000, None),
+    (16, 300_000_000, 19, 3_000_001, "22"),
 ])
-def test_round6_probe_on_build_image(vbf, ora, L, n, chunk_log2):
+def test_round6_probe_on_build_image(vbf, ora, L, m, k, n, chunk_log2):
     """The round-6 probe (vbf_probe_pu.hip: the build's unpadded tile image, padded result bits,
-    posv) at config 5's shape -- m = 2^32 - 1 (the reference's saturated size, bf.rs:230-233),
-    k = 4 -- against the round-3 pipeline (VBF_PROBE_PU=0), the gather probe and the oracle: answers
-    and counts, half the batch positive; single keys, tile edges (6 532 keys per tile), several
-    chunks.  Anchor: contains(), bf.rs:95-105."""
+    posv) against the earlier pipelines (VBF_PROBE_PU=0: round 3 at m = 2^32 - 1, the round-4
+    position-table pipeline at k = 10 / 19), the gather probe and the oracle: answers and counts,
+    half the batch positive.  Config 5's shape (m = 2^32 - 1, the reference's saturated size,
+    bf.rs:230-233; k = 4) with single keys, tile edges (6 532 keys per tile) and several chunks;
+    k = 10 / 19 with one segment (m = 5 000: every tile's runs split over many workgroups), the
+    largest m of the path (2^31) and several chunks.  Anchor: contains(), bf.rs:95-105."""
     import torch
     from velarixdb_amd._lib import call
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
-    m, k = 4_294_967_295, 4
     keys, offs, stride = _keys(torch, L, n, 0x5EED0161)
     words = torch.zeros((m + 31) // 32, dtype=torch.int32, device="cuda:0")
     half = max(1, n // 2)
@@ -210,7 +221,7 @@ def test_round6_probe_skewed_runs(vbf, ora):
     answers in every result byte)."""
     import torch
     from velarixdb_amd._lib import call
-    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
     m, k, L, n = 4_294_967_295, 4, 32, 2_000_000
     base, _, _ = _keys(torch, L, 5, 0x5EED0171)
     idx = torch.arange(n, device="cuda:0") % 5

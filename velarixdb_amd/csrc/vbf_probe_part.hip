@@ -108,7 +108,10 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg(const uint32_t* tiles, co
             for (int g = 0; g < NG; ++g) {
                 const uint32_t st = bt.be[g] & 0xFFFFu, len = (bt.be[g] >> 16) - st;
                 const uint64_t t = t0 + g * 8 + grp;
-                if (q8 < len) res[(t * pl.cap + st + q8) >> 3] = (uint8_t)test8(bt.a[g], bt.b[g]);
+                if (q8 < len) {
+                    const uint32_t r = test8(bt.a[g], bt.b[g]);
+                    if (r != 0xFFu) res[(t * pl.cap + st + q8) >> 3] = (uint8_t)r;  // bytes start all ones
+                }
             }
 #pragma unroll
             for (int g = 0; g < NG; ++g) {  // runs longer than 64 entries
@@ -117,8 +120,9 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg(const uint32_t* tiles, co
 #pragma unroll 1
                 for (uint32_t x = st + q8 + 64; x < st + len; x += 64) {
                     const uint32_t* run = tiles + t * pl.cap + x;
-                    res[(t * pl.cap + x) >> 3] =
-                        (uint8_t)test8(*reinterpret_cast<const uint4*>(run), *reinterpret_cast<const uint4*>(run + 4));
+                    const uint32_t r =
+                        test8(*reinterpret_cast<const uint4*>(run), *reinterpret_cast<const uint4*>(run + 4));
+                    if (r != 0xFFu) res[(t * pl.cap + x) >> 3] = (uint8_t)r;
                 }
             }
         };
@@ -152,7 +156,8 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg(const uint32_t* tiles, co
             for (uint32_t x = beg + q8; x < end; x += 64) {
                 const uint4 a = *reinterpret_cast<const uint4*>(run + x);
                 const uint4 b = *reinterpret_cast<const uint4*>(run + x + 4);
-                res[((uint64_t)t * pl.cap + x) >> 3] = (uint8_t)test8(a, b);
+                const uint32_t r = test8(a, b);
+                if (r != 0xFFu) res[((uint64_t)t * pl.cap + x) >> 3] = (uint8_t)r;
             }
         }
     }
@@ -254,7 +259,7 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg2(const uint32_t* tiles, c
             const uint32_t off = ((w[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) | (((nib >> (4 * c)) & 15u) << 16);
             r |= ((bitmap[off >> 5] >> (off & 31)) & 1u) << c;
         }
-        res[(uint64_t)t * rstride + gi] = (uint8_t)r;
+        if (r != 0xFFu) res[(uint64_t)t * rstride + gi] = (uint8_t)r;  // bytes start all ones
     };
     const uint32_t wstep = (kPBlock / 64) * 64;
     struct FB {
@@ -449,6 +454,10 @@ static hipError_t launch_probe_pp(const KeyBatch& kb, uint32_t m, uint32_t k, co
         if (err != hipSuccess) return err;
         phase_end(kPhaseProbePack, s);
         phase_begin(kPhaseProbeSeg, s);
+        // every result bit starts "pass": the segment pass stores only bytes holding a failing entry
+        // (a positive probe stores none; the scattered byte stores cost the segment pass most)
+        err = hipMemsetAsync(res, 0xFF, (uint64_t)ntiles * (pl.CPg / 8), s);
+        if (err != hipSuccess) return err;
         const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
         hipLaunchKernelGGL(k_probe_seg2<4>, dim3(pl.nseg * G), dim3(kPBlock), 0, s, tiles, endsT, ntiles, pl, G, words,
                            res);
@@ -605,6 +614,8 @@ hipError_t launch_probe_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         launch_transpose_u16(ends, endsT, ntiles, pl.nseg, s);
         phase_end(kPhaseProbePack, s);
         phase_begin(kPhaseProbeSeg, s);
+        err = hipMemsetAsync(res, 0xFF, (uint64_t)ntiles * (pl.cap / 8), s);  // bytes start all ones
+        if (err != hipSuccess) return err;
         const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
         uint32_t nfull = G > 1 ? 0u : pl.nseg, P = G;
         if (G == 1 && probe_split_enabled()) {

@@ -110,13 +110,17 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg3(const uint32_t* tiles, c
         return c < f.total ? 1u : 0u;
     };
     // result byte j of run [st, en) with padded begin pb: entries st + 8j .. st + 8j + 7 = the high
-    // bits of group j from slot sh = st & 7 on and the low bits of group j + 1
+    // bits of group j from slot sh = st & 7 on and the low bits of group j + 1.  The result bytes
+    // start all ones (the launcher fills them), so only a byte with a clear bit -- an entry whose
+    // filter bit is 0 -- is stored: a positive sweep stores nothing, and the scattered byte stores
+    // were what the segment pass waited on (one per run: 21.9 ms per 1B keys at config 5 against
+    // the build's 7.9 ms for the same runs)
     auto emit = [&](uint32_t t, uint32_t j, uint32_t rb, uint32_t re, uint32_t bits, uint32_t nbits) {
         const uint32_t st = rb & 0xFFFFu, len = (re & 0xFFFFu) - st, sh = st & 7u;
         if (8 * j >= len) return;
-        uint32_t v = (bits >> sh) | (nbits << (8 - sh));
-        if (len - 8 * j < 8) v &= (1u << (len - 8 * j)) - 1u;
-        res[(uint64_t)t * rstride + ((rb >> 16) >> 3) + j] = (uint8_t)v;
+        uint32_t v = ((bits >> sh) | (nbits << (8 - sh))) & 0xFFu;
+        if (len - 8 * j < 8) v = (v | (0xFFu << (len - 8 * j))) & 0xFFu;  // bits past the run: pass
+        if (v != 0xFFu) res[(uint64_t)t * rstride + ((rb >> 16) >> 3) + j] = (uint8_t)v;
     };
     // lane 63 of the last slot of a step: its run's next group belongs to the next step -- load it
     auto next_own = [&](uint32_t t, uint32_t gi, uint32_t j, uint32_t rb, uint32_t re) -> uint32_t {
@@ -242,18 +246,24 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, cons
 
 // ---- host side ----
 
-// The shapes U1 has kernels for: k = 4 at m = 2^32 - 1 (config 5: SAT remainders, packed counters,
-// the 512-thread shape with fourteen stash rounds = the build's 7 168-key tile), keys of a
-// compile-time length (16 / 32 / 8 / 24 bytes) hashed with the length prefix.  Other batches take
-// the round-3 pipeline; VBF_PROBE_PU = 0 keeps it for these too (A/B).
+// The shapes U1 has kernels for, keys of a compile-time length (16 / 32 / 8 / 24 bytes) hashed with
+// the length prefix (every Vec<u8> key):
+//   k = 4 at m = 2^32 - 1 (config 5: SAT remainders, the 1 024-thread shape, seven stash rounds);
+//   k = 10 and 19 (p = 1e-4, velarixdb's default) at m <= 2^31: the build's 512-thread
+//   one-lane-per-key shape with its full tile -- where the round-4 pipeline (vbf_probe_part.hip)
+//   reserves 7 entries of LDS per segment for run padding.
+// Other batches take the round-3 / round-4 pipelines; VBF_PROBE_PU = 0 keeps them for these too (A/B).
 static bool pu_shape(const PartPlan& pl, bool lp) {
-    return lp && pl.k == 4 && pl.m == 0xFFFFFFFFull && !pl.c16 && pl.k1v == 0 && pl.kc == 0 && pl.ends_t;
+    if (!lp || pl.c16 || pl.kc || !pl.ends_t) return false;
+    if (pl.k == 4) return pl.m == 0xFFFFFFFFull && pl.k1v == 0;
+    return (pl.k == 10 || pl.k == 19) && pl.m <= (1ull << 31) && pl.k1v == 1;
 }
 
 bool probe_pu_enabled(uint32_t m, uint32_t k, bool lp, bool fixed) {
     const char* e = getenv("VBF_PROBE_PU");  // read per call (A/B)
     static const int sat = [] { const char* v = getenv("VBF_SAT"); return v ? atoi(v) : 1; }();
-    if ((e && atoi(e) == 0) || !sat || !lp || !fixed || k != 4 || m != 0xFFFFFFFFu) return false;
+    if ((e && atoi(e) == 0) || !lp || !fixed || m == 0) return false;
+    if (!((k == 4 && m == 0xFFFFFFFFu && sat) || ((k == 10 || k == 19) && m <= (1u << 31)))) return false;
     const PartPlan pl = make_probe_pu_plan(m, k, fixed, lp);
     // padded ends must fit u16 (C + 7 per segment)
     return pu_shape(pl, lp) && pl.C + 7ull * pl.nseg <= 65535 && pl.CP <= 65535;
@@ -286,7 +296,7 @@ static PuLayout pu_layout(const PartPlan& pl, bool fixed, uint64_t n) {
     L.o_ends = align256(L.max_tiles * pl.tile_words * 4);
     L.o_res = align256(L.o_ends + ntS * pl.nseg * 4);
     L.o_pos = align256(L.o_res + L.max_tiles * L.rstride);
-    L.o_part = align256(L.o_pos + L.max_tiles * (uint64_t)L.pairs * (pl.k1v ? 512 : kPBlock) * 4);
+    L.o_part = align256(L.o_pos + L.max_tiles * (uint64_t)L.pairs * (uint32_t)sh.bs * 4);
     L.bytes = L.o_part + L.max_tiles * 4 + 256;
     return L;
 }
@@ -298,7 +308,9 @@ uint64_t probe_pu_workspace_bytes(uint64_t n, uint32_t m, uint32_t k, bool lp) {
 template <int FMT>
 static hipError_t launch_pu_pack(const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles,
                                  uint32_t* endsT, uint32_t* posv, hipStream_t s) {
-    auto fn = k_tile_pack<FMT, true, 4, false, false, 0, 0, kSegBits, 2, true>;
+    auto fn = pl.k == 4    ? k_tile_pack<FMT, true, 4, false, false, 0, 0, kSegBits, 2, true>
+              : pl.k == 10 ? k_tile_pack<FMT, true, 10, true, false, 1, 0, kSegBits, 2, false>
+                           : k_tile_pack<FMT, true, 19, true, false, 1, 0, kSegBits, 2, false>;
     // the segment counters sit at LDS address 0: no static LDS may precede them
     hipFuncAttributes fa{};
     hipError_t err = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fn));
@@ -307,8 +319,8 @@ static hipError_t launch_pu_pack(const DevKeys& dk, const PartPlan& pl, uint32_t
         err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)pl.lds1);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, reinterpret_cast<uint16_t*>(endsT),
-                       reinterpret_cast<uint16_t*>(posv));
+    hipLaunchKernelGGL(fn, dim3(ntiles), dim3(pl.k1v ? 512 : kPBlock), pl.lds1, s, dk, pl, tiles,
+                       reinterpret_cast<uint16_t*>(endsT), reinterpret_cast<uint16_t*>(posv));
     return hipGetLastError();
 }
 
@@ -347,23 +359,30 @@ hipError_t launch_probe_pu(const KeyBatch& kb, uint32_t m, uint32_t k, const uin
         if (err != hipSuccess) return err;
         phase_end(kPhaseProbePack, s);
         phase_begin(kPhaseProbeSeg, s);
+        // every result bit starts "pass"; the segment pass stores only bytes with a failing entry
+        err = hipMemsetAsync(res, 0xFF, (uint64_t)ntiles * L.rstride, s);
+        if (err != hipSuccess) return err;
         const uint32_t G = std::max<uint32_t>(1, std::min<uint32_t>(ntiles, (512 + pl.nseg - 1) / pl.nseg));
         hipLaunchKernelGGL(k_probe_seg3<4>, dim3(pl.nseg * G), dim3(kPBlock), 0, s, tiles, endsT, ntiles, pl, G, words,
                            res, L.rstride);
         phase_end(kPhaseProbeSeg, s);
         phase_begin(kPhaseProbeOut, s);
-        // KPT = ceil(KT / 1024) keys per thread (7 for the 6 531-key tile); posv rows of 1 024 lanes
-        if ((pl.KT + kPBlock - 1) / kPBlock > 7) return hipErrorInvalidValue;
+        // KPT = ceil(KT / 1024) keys per thread (k = 4: 7 for the 6 532-key tile, posv rows of 1 024
+        // lanes; k = 10: 3 for 3 072, k = 19: 2 for 1 536, rows of 512)
+        auto pick = [&]<int OUT>() {
+            return pl.k == 4 ? k_probe_out3<4, kPBlock, 7, OUT> : pl.k == 10 ? k_probe_out3<10, 512, 3, OUT>
+                                                                            : k_probe_out3<19, 512, 2, OUT>;
+        };
+        const uint32_t kpt_max = pl.k == 4 ? 7u : pl.k == 10 ? 3u : 2u;
+        if ((pl.KT + kPBlock - 1) / kPBlock > kpt_max) return hipErrorInvalidValue;
         if (count) {
-            auto fn = k_probe_out3<4, kPBlock, 7, 1>;
-            hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs, L.rstride, cn, nullptr,
-                               partial);
+            hipLaunchKernelGGL(pick.template operator()<1>(), dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs,
+                               L.rstride, cn, nullptr, partial);
             err = launch_count_finish(partial, ntiles, count, s);
             if (err != hipSuccess) return err;
         } else {
-            auto fn = k_probe_out3<4, kPBlock, 7, 0>;
-            hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs, L.rstride, cn, out + lo,
-                               nullptr);
+            hipLaunchKernelGGL(pick.template operator()<0>(), dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs,
+                               L.rstride, cn, out + lo, nullptr);
         }
         phase_end(kPhaseProbeOut, s);
         err = hipGetLastError();
