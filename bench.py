@@ -163,8 +163,10 @@ def pmc_traffic(name, kernel=None):
             with open(path) as f:
                 d = json.load(f)
             per_kernel = None
-            # round 4 added defaulted template arguments (KC, SB, POS, SAT) to k_tile_pack's name
-            norm = lambda x: x.replace(", 0, 20, false, false>", ">").replace(", 0, 20, false>", ">")
+            # round 4 added defaulted template arguments (KC, SB, POS, SAT) to k_tile_pack's name;
+            # round 6 made POS an int (0 = the build, 2 = the round-6 probe pack)
+            norm = lambda x: (x.replace(", 0, 20, false, false>", ">").replace(", 0, 20, 0, false>", ">")
+                              .replace(", 0, 20, false>", ">").replace(", 0, 20, 0>", ">"))
             for kname, kv in d.get("kernels", {}).items():
                 if kernel and norm(kernel) in norm(kname):
                     per_kernel = kv["read_bytes"] + kv["write_bytes"]

@@ -351,8 +351,22 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out2(const uint8_t* res, cons
     const uint32_t nk = (uint32_t)std::min<uint64_t>(pl.KT, n - key0);
     const uint32_t rbytes = pl.CPg / 8;
     const uint8_t* src = res + (uint64_t)tile * rbytes;
-    for (uint32_t b = tid; b < rbytes; b += kPBlock) reinterpret_cast<uint8_t*>(rl32)[b] = src[b];
-    __syncthreads();
+    uint32_t all = 0xFFu;
+    for (uint32_t b = tid; b < rbytes; b += kPBlock) {
+        const uint8_t v = src[b];
+        reinterpret_cast<uint8_t*>(rl32)[b] = v;
+        all &= v;
+    }
+    // no failing entry in the tile (the segment pass stored none of its result bytes): every key
+    // passes without reading the position table
+    if (__syncthreads_and(all == 0xFFu)) {
+        if constexpr (OUT == 0) {
+            for (uint32_t l = tid; l < nk; l += kPBlock) out[key0 + l] = 1;
+        } else if (tid == 0) {
+            partial[blockIdx.x] = nk;
+        }
+        return;
+    }
     const uint32_t* pt = posv + (uint64_t)tile * pairs * 512;
     constexpr int NW = K / 2 + 1;
     uint32_t wv[KPT][NW];

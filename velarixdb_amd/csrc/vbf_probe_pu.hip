@@ -197,8 +197,22 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, cons
     const uint32_t nk = (uint32_t)std::min<uint64_t>(pl.KT, n - key0);
     // rbytes is a multiple of 4 and res 256-byte aligned (pu_layout): dword copies
     const uint32_t* src = reinterpret_cast<const uint32_t*>(res + (uint64_t)tile * rbytes);
-    for (uint32_t w = tid; w < rbytes / 4; w += kPBlock) rl32[w] = src[w];
-    __syncthreads();
+    uint32_t all = 0xFFFFFFFFu;
+    for (uint32_t w = tid; w < rbytes / 4; w += kPBlock) {
+        const uint32_t v = src[w];
+        rl32[w] = v;
+        all &= v;
+    }
+    // no entry of the tile failed (the segment pass stored none of its result bytes): every key
+    // passes, and the position table need not be read -- a positive sweep's common case
+    if (__syncthreads_and(all == 0xFFFFFFFFu)) {
+        if constexpr (OUT == 0) {
+            for (uint32_t l = tid; l < nk; l += kPBlock) out[key0 + l] = 1;
+        } else if (tid == 0) {
+            partial[blockIdx.x] = nk;
+        }
+        return;
+    }
     const uint32_t* pt = posv + (uint64_t)tile * pairs * BS;
     constexpr int NW = K / 2 + 1;
     uint32_t wv[KPT][NW];
