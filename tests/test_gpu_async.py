@@ -549,3 +549,35 @@ def test_words_dev_read_keeps_the_mirror(vbf, ora):
     # ... while the writable pointer makes every host read copy the words again
     f.words_dev_ptr()
     assert f.contains_batch(HostBatch(neg, None, L, 64, 1)).all()
+
+
+@pytest.mark.parametrize("n", [300_000, 20_000_000])  # one staged key chunk; five (64 MiB each)
+def test_compaction_path_allocates_no_host_words_and_builds_fresh(vbf, ora, n):
+    """VERDICT r05 #4, the patched build_filter_from_entries: new on the
+    host (bf.rs:62-81) -> migrate(AUTO) -> set_host_async -> words.  The host-side `new` allocates
+    no bit array and the move to the GPU copies none (vbf_filter_host_bytes stays 0); the device
+    words of the pristine filter are zeroed asynchronously and the queued build's first chunk is
+    the fused fresh build, the later chunks OR in after it; the words equal the oracle's.  A
+    pristine device filter read before any set is all zeros (the asynchronous zero fill is
+    ordered before every use, the device pointer included)."""
+    from velarixdb_amd.filter import AUTO, HOST
+    from velarixdb_amd.keys import HostBatch
+    L = 16
+    h = ora.gen_fixed(0x5EED0E80, 0, n, L)
+    f = vbf.BloomFilter(1e-4, n, device=HOST)
+    assert f.host_bytes == 0
+    f.migrate(AUTO)
+    assert not f.host_resident and f.host_bytes == 0
+    f.set_many_async(HostBatch(h, None, L, n, 1), zero_copy=True)
+    f.sync()
+    assert np.array_equal(f.words(), _oracle_words(ora, 0x5EED0E80, n, f.num_bits(), f.no_of_hash_func))
+    assert f.no_of_elements == n
+    for read in ("pointer", "words"):
+        g = vbf.BloomFilter(0.01, 1_000_000, device=HOST)
+        g.migrate(AUTO)
+        if read == "pointer":  # the zero fill is done before the pointer is handed out
+            c = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+            vbf._lib.call("vbf_popcount_dev", ctypes.c_void_p(g.words_dev_read_ptr()), g.num_words(),
+                          ctypes.c_void_p(c.data_ptr()), None)
+            assert int(c.item()) == 0
+        assert not g.words().any() and not g.contains(b"never set") and g.host_bytes == g.num_words() * 4
