@@ -40,6 +40,8 @@ for s in $STEPS; do
             (cd /tmp && run pmc_${tag}_$i 240 rocprofv3 --pmc $c -d "$OUT/meas/${tag}_$i" -o run --output-format csv -- $B $a) || exit $?
           done
         done ;;
+    benchq19) run bench_k19q 300 python bench.py --no-cpu-baseline --bits-per-key 19 --steps 50 ;;
+    prof5ab) (cd /tmp && run prof5ab 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof5ab" -o run -- python3 "$ROOT/bench.py" --config 5 --steps 3 --warmup 1 --no-cpu-baseline --probe-ab) || exit $? ;;
     sel)    run pytest_sel 1200 python -u -m pytest $PYTEST_ARGS -x -v -m gpu --timeout 300 --timeout-method thread ;;
     bench5ab) run bench_cfg5_ab 900 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline --probe-ab ;;
     smoke)  run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

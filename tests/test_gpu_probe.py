@@ -184,6 +184,10 @@ SAT = 4_294_967_295
     (16, 1_000_000_000, 10, 2_000_000, None), (16, 1_900_000_000, 19, 1_000_000, None),
     (32, 1 << 31, 19, 600_000, None), (8, 5_000, 10, 300_000, None), (24, 70_000_000, 10, 1_200_000, None),
     (16, 300_000_000, 19, 3_000_001, "22"),
+    # runtime-k classes (k outside {4, 9, 10, 19}) at m <= 2^31: every class, the largest m
+    (16, 300_000_007, 14, 1_000_000, None), (32, 50_000_017, 7, 600_000, None), (8, 40_000_003, 32, 200_000, None),
+    (24, 100_000_007, 23, 400_000, None), (16, 1 << 31, 12, 500_000, None), (16, 200_000_003, 5, 900_000, None),
+    (32, 150_000_001, 21, 300_000, "22"),
 ])
 def test_round6_probe_on_build_image(vbf, ora, L, m, k, n, chunk_log2):
     """The round-6 probe (vbf_probe_pu.hip: the build's unpadded tile image, padded result bits,
@@ -192,7 +196,8 @@ def test_round6_probe_on_build_image(vbf, ora, L, m, k, n, chunk_log2):
     half the batch positive.  Config 5's shape (m = 2^32 - 1, the reference's saturated size,
     bf.rs:230-233; k = 4) with single keys, tile edges (6 532 keys per tile) and several chunks;
     k = 10 / 19 with one segment (m = 5 000: every tile's runs split over many workgroups), the
-    largest m of the path (2^31) and several chunks.  Anchor: contains(), bf.rs:95-105."""
+    largest m of the path (2^31) and several chunks; every runtime-k class (the K1 class kernels with
+    the class's slots per key, k at run time).  Anchor: contains(), bf.rs:95-105."""
     import torch
     from velarixdb_amd._lib import call
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None

@@ -6,7 +6,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["vbf_kernels.hip", "vbf_partition.hip", "vbf_partition_rk_a.hip", "vbf_partition_rk_b.hip", "vbf_partition_rk_c.hip", "vbf_partition_rk_d.hip", "vbf_partition_sat.hip", "vbf_partition_k1_a.hip", "vbf_partition_k1_b.hip", "vbf_partition_k1_c.hip", "vbf_probe_part.hip", "vbf_probe_part_rk_a.hip", "vbf_probe_part_rk_b.hip", "vbf_probe_part_rk_c.hip", "vbf_probe_part_rk_d.hip", "vbf_probe_pu.hip", "vbf_sst.hip", "vbf_multi.hip", "vbf_multi_part.hip", "vbf_compact.hip", "vbf_api.hip"]
+SOURCES = ["vbf_kernels.hip", "vbf_partition.hip", "vbf_partition_rk_a.hip", "vbf_partition_rk_b.hip", "vbf_partition_rk_c.hip", "vbf_partition_rk_d.hip", "vbf_partition_sat.hip", "vbf_partition_k1_a.hip", "vbf_partition_k1_b.hip", "vbf_partition_k1_c.hip", "vbf_probe_part.hip", "vbf_probe_part_rk_a.hip", "vbf_probe_part_rk_b.hip", "vbf_probe_part_rk_c.hip", "vbf_probe_part_rk_d.hip", "vbf_probe_pu.hip", "vbf_probe_pu_rk_a.hip", "vbf_probe_pu_rk_b.hip", "vbf_sst.hip", "vbf_multi.hip", "vbf_multi_part.hip", "vbf_compact.hip", "vbf_api.hip"]
 OUT = os.path.join(HERE, "libvbf.so")
 ARCH = os.environ.get("VBF_OFFLOAD_ARCH", "gfx950")
 

@@ -17,8 +17,21 @@
 //                             through posv and ANDed: the answer byte, or the tile's hit count.
 // The same hashing as the build, the build's run count for the segment pass, and no key id stored.
 #include "vbf_tile_pack.hpp"
+#include "vbf_tile_pack_rk.hpp"
 
 namespace vbf {
+
+// U1 for the runtime-k classes (k outside {4, 9, 10, 19}, m <= 2^31, compile-time key lengths):
+// vbf_probe_pu_rk_a.hip (classes 5, 8, 12) and _b (16, 21, 24, 32), compiled in parallel.
+hipError_t launch_pu_pack_class_a(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles,
+                                  uint32_t* endsT, uint32_t* posv, hipStream_t s);
+hipError_t launch_pu_pack_class_b(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles,
+                                  uint32_t* endsT, uint32_t* posv, hipStream_t s);
+static hipError_t launch_pu_pack_class(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles,
+                                       uint32_t* tiles, uint32_t* endsT, uint32_t* posv, hipStream_t s) {
+    return pl.kc <= 12 ? launch_pu_pack_class_a(fmt, dk, pl, ntiles, tiles, endsT, posv, s)
+                       : launch_pu_pack_class_b(fmt, dk, pl, ntiles, tiles, endsT, posv, s);
+}
 
 // U3.  Blocks: G consecutive tile ranges per segment, XCD-aware (neighbouring segments on one XCD
 // share the L2 lines their short runs sit in, as in k_seg_or).
@@ -185,7 +198,8 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg3(const uint32_t* tiles, c
 // U4 (OUT 0: answer bytes, 1: hits of the tile -> partial[tile]).  posv: u16 pairs per pair of stash
 // slots, [tile][slot / 2][lane of BS]; key l of the tile = round l / BS on lane l % BS, its seeds in
 // slots round * K + i.  K compile-time: a lane issues the position loads of its KPT keys together.
-template <int K, int BS, int KPT, int OUT>
+// RK: K is a runtime-k class (the stash slots per key); the key's k = pl.k <= K seeds are ANDed.
+template <int K, int BS, int KPT, int OUT, bool RK = false>
 __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, const uint32_t* posv, PartPlan pl,
                                                         uint32_t pairs, uint32_t rbytes, uint64_t n, uint8_t* out,
                                                         uint32_t* partial) {
@@ -238,10 +252,12 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, cons
         const uint32_t odd = ((l / BS) * K) & 1u;
         if (odd) {
 #pragma unroll
-            for (int i = 0; i < K; ++i) ok &= bit_at(x, i, 1u);
+            for (int i = 0; i < K; ++i)
+                if (!RK || (uint32_t)i < pl.k) ok &= bit_at(x, i, 1u);
         } else {
 #pragma unroll
-            for (int i = 0; i < K; ++i) ok &= bit_at(x, i, 0u);
+            for (int i = 0; i < K; ++i)
+                if (!RK || (uint32_t)i < pl.k) ok &= bit_at(x, i, 0u);
         }
         if constexpr (OUT == 0) out[key0 + l] = (uint8_t)ok;
         else hits += ok;
@@ -268,7 +284,8 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, cons
 //   reserves 7 entries of LDS per segment for run padding.
 // Other batches take the round-3 / round-4 pipelines; VBF_PROBE_PU = 0 keeps them for these too (A/B).
 static bool pu_shape(const PartPlan& pl, bool lp) {
-    if (!lp || pl.c16 || pl.kc || !pl.ends_t) return false;
+    if (!lp || pl.c16 || !pl.ends_t) return false;
+    if (pl.kc) return pl.m <= (1ull << 31) && pl.k1v == 1;  // a runtime-k class (round 6, late)
     if (pl.k == 4) return pl.m == 0xFFFFFFFFull && pl.k1v == 0;
     return (pl.k == 10 || pl.k == 19) && pl.m <= (1ull << 31) && pl.k1v == 1;
 }
@@ -277,7 +294,8 @@ bool probe_pu_enabled(uint32_t m, uint32_t k, bool lp, bool fixed) {
     const char* e = getenv("VBF_PROBE_PU");  // read per call (A/B)
     static const int sat = [] { const char* v = getenv("VBF_SAT"); return v ? atoi(v) : 1; }();
     if ((e && atoi(e) == 0) || !lp || !fixed || m == 0) return false;
-    if (!((k == 4 && m == 0xFFFFFFFFu && sat) || ((k == 10 || k == 19) && m <= (1u << 31)))) return false;
+    const bool cls = k != 4 && k != 9 && k != 10 && k != 19 && tile_pack_class(k) != 0;
+    if (!((k == 4 && m == 0xFFFFFFFFu && sat) || ((k == 10 || k == 19 || cls) && m <= (1u << 31)))) return false;
     const PartPlan pl = make_probe_pu_plan(m, k, fixed, lp);
     // padded ends must fit u16 (C + 7 per segment)
     return pu_shape(pl, lp) && pl.C + 7ull * pl.nseg <= 65535 && pl.CP <= 65535;
@@ -303,7 +321,7 @@ static PuLayout pu_layout(const PartPlan& pl, bool fixed, uint64_t n) {
     L.max_tiles = (L.chunk_keys + pl.KT - 1) / pl.KT;
     const uint64_t ntS = (L.max_tiles + 7) & ~7ull;
     // stash slots per lane of the kernel (SPL = 1): its compile-time rounds x seeds
-    const K1Shape sh = k1_shape((int)pl.k, fixed, (int)pl.k1v);
+    const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : pl.k), fixed, (int)pl.k1v);
     L.pairs = (uint32_t)(sh.rounds * sh.kl + 1) / 2;
     // result bytes per tile: every run rounded up to whole bytes, <= (C + 7 * nseg) / 8, 4-aligned
     L.rstride = (uint32_t)(((pl.C + 7ull * pl.nseg + 7) / 8 + 3) & ~3ull);
@@ -363,7 +381,8 @@ hipError_t launch_probe_pu(const KeyBatch& kb, uint32_t m, uint32_t k, const uin
         pl.ntS = (ntiles + 7) & ~7u;
         hipError_t err = hipErrorInvalidValue;
         phase_begin(kPhaseProbePack, s);
-        switch (fmt) {
+        if (pl.kc) err = launch_pu_pack_class(fmt, dk, pl, ntiles, tiles, endsT, posv, s);
+        else switch (fmt) {
             case 16: err = launch_pu_pack<16>(dk, pl, ntiles, tiles, endsT, posv, s); break;
             case 32: err = launch_pu_pack<32>(dk, pl, ntiles, tiles, endsT, posv, s); break;
             case 8: err = launch_pu_pack<8>(dk, pl, ntiles, tiles, endsT, posv, s); break;
@@ -383,11 +402,23 @@ hipError_t launch_probe_pu(const KeyBatch& kb, uint32_t m, uint32_t k, const uin
         phase_begin(kPhaseProbeOut, s);
         // KPT = ceil(KT / 1024) keys per thread (k = 4: 7 for the 6 532-key tile, posv rows of 1 024
         // lanes; k = 10: 3 for 3 072, k = 19: 2 for 1 536, rows of 512)
+        // classes: K = the class's slots per key, k at run time; KPT from the class's rounds of 512
         auto pick = [&]<int OUT>() {
+            switch (pl.kc) {
+                case 5: return k_probe_out3<5, 512, 3, OUT, true>;
+                case 8: return k_probe_out3<8, 512, 3, OUT, true>;
+                case 12: return k_probe_out3<12, 512, 3, OUT, true>;
+                case 16: return k_probe_out3<16, 512, 2, OUT, true>;
+                case 21: return k_probe_out3<21, 512, 2, OUT, true>;
+                case 24: return k_probe_out3<24, 512, 1, OUT, true>;
+                case 32: return k_probe_out3<32, 512, 1, OUT, true>;
+                default: break;
+            }
             return pl.k == 4 ? k_probe_out3<4, kPBlock, 7, OUT> : pl.k == 10 ? k_probe_out3<10, 512, 3, OUT>
                                                                             : k_probe_out3<19, 512, 2, OUT>;
         };
-        const uint32_t kpt_max = pl.k == 4 ? 7u : pl.k == 10 ? 3u : 2u;
+        const uint32_t kpt_max = pl.kc ? (pl.kc <= 12 ? 3u : pl.kc <= 21 ? 2u : 1u)
+                                       : pl.k == 4 ? 7u : pl.k == 10 ? 3u : 2u;
         if ((pl.KT + kPBlock - 1) / kPBlock > kpt_max) return hipErrorInvalidValue;
         if (count) {
             hipLaunchKernelGGL(pick.template operator()<1>(), dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs,
