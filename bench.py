@@ -128,10 +128,10 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32
 
 # rocprofv3 names of the build's kernels, and the summary of the same command, per (key bytes, k)
 ROCPROF = {
-    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true, false, 1, 0, 20, false, false>",
-                "seg_or": "k_seg_or<6, 1024, 5, 8>"}, "profiles/r05/bench_default_kernel_stats.csv"),
-    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true, false, 1, 0, 20, false, false>",
-                "seg_or": "k_seg_or<6, 1024, 4, 8>"}, "profiles/r05/bench_k19_kernel_stats.csv"),
+    (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true, false, 1, 0, 20, 0, false>",
+                "seg_or": "k_seg_or<6, 1024, 5, 8>"}, "profiles/r06/bench_default_kernel_stats.csv"),
+    (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true, false, 1, 0, 20, 0, false>",
+                "seg_or": "k_seg_or<6, 1024, 4, 8>"}, "profiles/r06/bench_k19_kernel_stats.csv"),
 }
 
 

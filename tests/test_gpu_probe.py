@@ -188,6 +188,11 @@ SAT = 4_294_967_295
     (16, 300_000_007, 14, 1_000_000, None), (32, 50_000_017, 7, 600_000, None), (8, 40_000_003, 32, 200_000, None),
     (24, 100_000_007, 23, 400_000, None), (16, 1 << 31, 12, 500_000, None), (16, 200_000_003, 5, 900_000, None),
     (32, 150_000_001, 21, 300_000, "22"),
+    # runtime key lengths: the offsets layout (keys dealt to lanes in length order; the answers go
+    # back through the slot -> key map) and an odd fixed stride (13 B: the runtime-stride layout)
+    (None, SAT, 4, 800_000, None), (None, 1_000_000_000, 10, 1_000_000, None), (None, 1_900_000_000, 19, 500_000, None),
+    (None, 300_000_007, 14, 500_000, None), (None, 500_000_000, 10, 2_000_000, "22"), (13, 1_000_000_000, 10, 700_000, None),
+    (13, SAT, 4, 500_000, None),
 ])
 def test_round6_probe_on_build_image(vbf, ora, L, m, k, n, chunk_log2):
     """The round-6 probe (vbf_probe_pu.hip: the build's unpadded tile image, padded result bits,
@@ -197,7 +202,8 @@ def test_round6_probe_on_build_image(vbf, ora, L, m, k, n, chunk_log2):
     bf.rs:230-233; k = 4) with single keys, tile edges (6 532 keys per tile) and several chunks;
     k = 10 / 19 with one segment (m = 5 000: every tile's runs split over many workgroups), the
     largest m of the path (2^31) and several chunks; every runtime-k class (the K1 class kernels with
-    the class's slots per key, k at run time).  Anchor: contains(), bf.rs:95-105."""
+    the class's slots per key, k at run time); variable-length keys (the pack's length order, the
+    answers mapped back to key order) and an odd fixed stride.  Anchor: contains(), bf.rs:95-105."""
     import torch
     from velarixdb_amd._lib import call
     P = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -215,7 +221,13 @@ def test_round6_probe_on_build_image(vbf, ora, L, m, k, n, chunk_log2):
     assert pu[1] == r3[1] == int(pu[0].sum())
     assert pu[0][:half].all()
     sl = slice(max(0, half - 1000), min(n, half + 30000))
-    batch = vbf.pack_fixed(keys.cpu().numpy().reshape(n, L)[sl], 1)
+    if offs is None:
+        batch = vbf.pack_fixed(keys.cpu().numpy().reshape(n, L)[sl], 1)
+    else:
+        o_h = offs.cpu().numpy().view(np.uint64)
+        kb = keys.cpu().numpy()
+        lo, hi = int(o_h[sl.start]), int(o_h[sl.stop])
+        batch = vbf.pack_offsets(kb[lo:hi], o_h[sl.start:sl.stop + 1] - lo, 1)
     assert np.array_equal(ora.probe(batch, m, k, words.cpu().numpy().view(np.uint32)).astype(np.uint8), pu[0][sl])
 
 
