@@ -657,8 +657,7 @@ PartPlan make_group_plan(uint32_t m, uint32_t k, bool fixed, int sb) { return ma
 
 PartPlan make_probe_pu_plan(uint32_t m, uint32_t k, bool fixed, bool lp) {
     PartPlan pl = make_plan(m, k, fixed, lp, 0, true);
-    pl.len_order = 0;  // posv maps lane slots to keys in key order
-    pl.stage_keys = 0;
+    pl.stage_keys = 0;  // the tile image holds the length order's perm only (written out before placement)
     return pl;
 }
 

@@ -21,7 +21,7 @@
 
 namespace vbf {
 
-// U1 for the runtime-k classes (k outside {4, 9, 10, 19}, m <= 2^31, compile-time key lengths):
+// U1 for the runtime-k classes (k outside {4, 9, 10, 19}, m <= 2^31, every key layout):
 // vbf_probe_pu_rk_a.hip (classes 5, 8, 12) and _b (16, 21, 24, 32), compiled in parallel.
 hipError_t launch_pu_pack_class_a(int fmt, const DevKeys& dk, const PartPlan& pl, uint32_t ntiles, uint32_t* tiles,
                                   uint32_t* endsT, uint32_t* posv, hipStream_t s);
@@ -199,7 +199,8 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg3(const uint32_t* tiles, c
 // slots, [tile][slot / 2][lane of BS]; key l of the tile = round l / BS on lane l % BS, its seeds in
 // slots round * K + i.  K compile-time: a lane issues the position loads of its KPT keys together.
 // RK: K is a runtime-k class (the stash slots per key); the key's k = pl.k <= K seeds are ANDed.
-template <int K, int BS, int KPT, int OUT, bool RK = false>
+// PERM: the pack dealt the keys to lanes in length order (offsets layout): slot l is key perm[l].
+template <int K, int BS, int KPT, int OUT, bool RK = false, bool PERM = false>
 __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, const uint32_t* posv, PartPlan pl,
                                                         uint32_t pairs, uint32_t rbytes, uint64_t n, uint8_t* out,
                                                         uint32_t* partial) {
@@ -259,8 +260,14 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, cons
             for (int i = 0; i < K; ++i)
                 if (!RK || (uint32_t)i < pl.k) ok &= bit_at(x, i, 0u);
         }
-        if constexpr (OUT == 0) out[key0 + l] = (uint8_t)ok;
-        else hits += ok;
+        if constexpr (OUT == 0) {
+            if constexpr (PERM)
+                out[key0 + reinterpret_cast<const uint16_t*>(posv)[pl.perm_off + (uint64_t)tile * pl.KT + l]] = (uint8_t)ok;
+            else
+                out[key0 + l] = (uint8_t)ok;
+        } else {
+            hits += ok;
+        }
     }
     if constexpr (OUT == 1) {
         for (int o = 32; o > 0; o >>= 1) hits += __shfl_down(hits, o);
@@ -276,8 +283,9 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, cons
 
 // ---- host side ----
 
-// The shapes U1 has kernels for, keys of a compile-time length (16 / 32 / 8 / 24 bytes) hashed with
-// the length prefix (every Vec<u8> key):
+// The shapes U1 has kernels for, every key layout (16 / 32 / 8 / 24-byte rows, any stride, offsets:
+// the length order's slot -> key map goes beside the positions) hashed with the length prefix
+// (every Vec<u8> key):
 //   k = 4 at m = 2^32 - 1 (config 5: SAT remainders, the 1 024-thread shape, seven stash rounds);
 //   k = 10 and 19 (p = 1e-4, velarixdb's default) at m <= 2^31: the build's 512-thread
 //   one-lane-per-key shape with its full tile -- where the round-4 pipeline (vbf_probe_part.hip)
@@ -293,8 +301,9 @@ static bool pu_shape(const PartPlan& pl, bool lp) {
 bool probe_pu_enabled(uint32_t m, uint32_t k, bool lp, bool fixed) {
     const char* e = getenv("VBF_PROBE_PU");  // read per call (A/B)
     static const int sat = [] { const char* v = getenv("VBF_SAT"); return v ? atoi(v) : 1; }();
-    if ((e && atoi(e) == 0) || !lp || !fixed || m == 0) return false;
+    if ((e && atoi(e) == 0) || !lp || m == 0) return false;
     const bool cls = k != 4 && k != 9 && k != 10 && k != 19 && tile_pack_class(k) != 0;
+    (void)fixed;
     if (!((k == 4 && m == 0xFFFFFFFFu && sat) || ((k == 10 || k == 19 || cls) && m <= (1u << 31)))) return false;
     const PartPlan pl = make_probe_pu_plan(m, k, fixed, lp);
     // padded ends must fit u16 (C + 7 per segment)
@@ -309,7 +318,7 @@ static uint64_t pu_chunk_idx() {
 }
 
 struct PuLayout {
-    uint64_t chunk_keys, max_tiles, o_ends, o_res, o_pos, o_part, bytes;
+    uint64_t chunk_keys, max_tiles, o_ends, o_res, o_pos, o_perm, o_part, bytes;
     uint32_t rstride, pairs;
 };
 
@@ -328,13 +337,17 @@ static PuLayout pu_layout(const PartPlan& pl, bool fixed, uint64_t n) {
     L.o_ends = align256(L.max_tiles * pl.tile_words * 4);
     L.o_res = align256(L.o_ends + ntS * pl.nseg * 4);
     L.o_pos = align256(L.o_res + L.max_tiles * L.rstride);
-    L.o_part = align256(L.o_pos + L.max_tiles * (uint64_t)L.pairs * (uint32_t)sh.bs * 4);
+    L.o_perm = align256(L.o_pos + L.max_tiles * (uint64_t)L.pairs * (uint32_t)sh.bs * 4);  // u16 [tile][KT]
+    L.o_part = align256(L.o_perm + (fixed ? 0 : L.max_tiles * (uint64_t)pl.KT * 2));
     L.bytes = L.o_part + L.max_tiles * 4 + 256;
     return L;
 }
 
 uint64_t probe_pu_workspace_bytes(uint64_t n, uint32_t m, uint32_t k, bool lp) {
-    return pu_layout(make_probe_pu_plan(m, k, true, lp), true, n).bytes;
+    uint64_t need = 0;
+    for (bool fixed : {true, false})
+        need = std::max(need, pu_layout(make_probe_pu_plan(m, k, fixed, lp), fixed, n).bytes);
+    return need;
 }
 
 template <int FMT>
@@ -369,6 +382,8 @@ hipError_t launch_probe_pu(const KeyBatch& kb, uint32_t m, uint32_t k, const uin
     uint32_t* endsT = reinterpret_cast<uint32_t*>(base + L.o_ends);
     uint8_t* res = reinterpret_cast<uint8_t*>(base + L.o_res);
     uint32_t* posv = reinterpret_cast<uint32_t*>(base + L.o_pos);
+    pl.perm_off = (L.o_perm - L.o_pos) / 2;  // the length order's slot -> key map (offsets layout)
+    const bool permuted = fmt < 0 && pl.len_order;
     uint32_t* partial = reinterpret_cast<uint32_t*>(base + L.o_part);
     for (uint64_t lo = 0; lo < kb.n; lo += L.chunk_keys) {
         const uint64_t cn = std::min<uint64_t>(L.chunk_keys, kb.n - lo);
@@ -387,7 +402,8 @@ hipError_t launch_probe_pu(const KeyBatch& kb, uint32_t m, uint32_t k, const uin
             case 32: err = launch_pu_pack<32>(dk, pl, ntiles, tiles, endsT, posv, s); break;
             case 8: err = launch_pu_pack<8>(dk, pl, ntiles, tiles, endsT, posv, s); break;
             case 24: err = launch_pu_pack<24>(dk, pl, ntiles, tiles, endsT, posv, s); break;
-            default: return hipErrorInvalidValue;
+            case -1: err = launch_pu_pack<-1>(dk, pl, ntiles, tiles, endsT, posv, s); break;
+            default: err = launch_pu_pack<0>(dk, pl, ntiles, tiles, endsT, posv, s); break;
         }
         if (err != hipSuccess) return err;
         phase_end(kPhaseProbePack, s);
@@ -403,30 +419,33 @@ hipError_t launch_probe_pu(const KeyBatch& kb, uint32_t m, uint32_t k, const uin
         // KPT = ceil(KT / 1024) keys per thread (k = 4: 7 for the 6 532-key tile, posv rows of 1 024
         // lanes; k = 10: 3 for 3 072, k = 19: 2 for 1 536, rows of 512)
         // classes: K = the class's slots per key, k at run time; KPT from the class's rounds of 512
-        auto pick = [&]<int OUT>() {
+        auto pick = [&]<int OUT, bool PM>() {
             switch (pl.kc) {
-                case 5: return k_probe_out3<5, 512, 3, OUT, true>;
-                case 8: return k_probe_out3<8, 512, 3, OUT, true>;
-                case 12: return k_probe_out3<12, 512, 3, OUT, true>;
-                case 16: return k_probe_out3<16, 512, 2, OUT, true>;
-                case 21: return k_probe_out3<21, 512, 2, OUT, true>;
-                case 24: return k_probe_out3<24, 512, 1, OUT, true>;
-                case 32: return k_probe_out3<32, 512, 1, OUT, true>;
+                case 5: return k_probe_out3<5, 512, 3, OUT, true, PM>;
+                case 8: return k_probe_out3<8, 512, 3, OUT, true, PM>;
+                case 12: return k_probe_out3<12, 512, 3, OUT, true, PM>;
+                case 16: return k_probe_out3<16, 512, 2, OUT, true, PM>;
+                case 21: return k_probe_out3<21, 512, 2, OUT, true, PM>;
+                case 24: return k_probe_out3<24, 512, 1, OUT, true, PM>;
+                case 32: return k_probe_out3<32, 512, 1, OUT, true, PM>;
                 default: break;
             }
-            return pl.k == 4 ? k_probe_out3<4, kPBlock, 7, OUT> : pl.k == 10 ? k_probe_out3<10, 512, 3, OUT>
-                                                                            : k_probe_out3<19, 512, 2, OUT>;
+            return pl.k == 4    ? k_probe_out3<4, kPBlock, 7, OUT, false, PM>
+                   : pl.k == 10 ? k_probe_out3<10, 512, 3, OUT, false, PM>
+                                : k_probe_out3<19, 512, 2, OUT, false, PM>;
         };
         const uint32_t kpt_max = pl.kc ? (pl.kc <= 12 ? 3u : pl.kc <= 21 ? 2u : 1u)
                                        : pl.k == 4 ? 7u : pl.k == 10 ? 3u : 2u;
         if ((pl.KT + kPBlock - 1) / kPBlock > kpt_max) return hipErrorInvalidValue;
         if (count) {
-            hipLaunchKernelGGL(pick.template operator()<1>(), dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs,
+            auto fn = pick.template operator()<1, false>();
+            hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs,
                                L.rstride, cn, nullptr, partial);
             err = launch_count_finish(partial, ntiles, count, s);
             if (err != hipSuccess) return err;
         } else {
-            hipLaunchKernelGGL(pick.template operator()<0>(), dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs,
+            auto fn = permuted ? pick.template operator()<0, true>() : pick.template operator()<0, false>();
+            hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), 0, s, res, posv, pl, L.pairs,
                                L.rstride, cn, out + lo, nullptr);
         }
         phase_end(kPhaseProbeOut, s);

@@ -1,5 +1,5 @@
 // vbf_probe_pu_rk_a.hip -- U1 of the round-6 probe (k_tile_pack<..., KC, POS = 2>) for the runtime-k
-// classes 5, 8 and 12, keys of a compile-time length hashed with the length prefix, m <= 2^31; a translation
+// classes 5, 8 and 12, every key layout (fixed and runtime lengths) hashed with the length prefix, m <= 2^31; a translation
 // unit of its own so the library builds in parallel (vbf_probe_pu.hip launches it).
 #include "vbf_tile_pack_rk.hpp"
 
@@ -31,7 +31,8 @@ hipError_t launch_pu_pack_class_a(int fmt, const DevKeys& dk, const PartPlan& pl
             case 32: err = launch_pu_one_class<32, KC>(dk, pl, ntiles, tiles, endsT, posv, s); break;
             case 8: err = launch_pu_one_class<8, KC>(dk, pl, ntiles, tiles, endsT, posv, s); break;
             case 24: err = launch_pu_one_class<24, KC>(dk, pl, ntiles, tiles, endsT, posv, s); break;
-            default: break;
+            case -1: err = launch_pu_one_class<-1, KC>(dk, pl, ntiles, tiles, endsT, posv, s); break;
+            default: err = launch_pu_one_class<0, KC>(dk, pl, ntiles, tiles, endsT, posv, s); break;
         }
     };
     one.template operator()<5>();

@@ -35,6 +35,7 @@ struct PartPlan {
     uint32_t nfull;       // K3: segments [0, nfull) one workgroup each; the rest split in P parts
     uint32_t P;
     uint64_t m, mu, nwords;
+    uint64_t perm_off;    // POS = 2 with the length order: u16 elements from posv to perm[tile][KT]
 };
 
 // Variable-length keys (offsets layout): a wave runs the prefix-absorb loop as long as its
@@ -334,6 +335,14 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
         }
     }
     __syncthreads();
+    if constexpr (POS == 2 && FMT < 0) {
+        // the probe answers keys in key order: the length order's slot -> key map goes out beside
+        // the positions (perm[tile][slot]) before the placement overwrites it
+        if (perm) {
+            uint16_t* pm = posv + pl.perm_off + (uint64_t)tile * pl.KT;
+            for (uint32_t l = tid; l < nk; l += BS) pm[l] = lo[l];
+        }
+    }
     // run starts; the 512-thread shape scans up to 8 counters per thread where m > 2^31
     // (up to 4 096 segments)
     constexpr int SPER = (V == 1 && !M31) ? 8 : 4;
