@@ -126,11 +126,14 @@ def multi_mode():
 @pytest.mark.parametrize("seed", [3, 4])
 def test_interleaved_groups_match_oracle(vbf, ora, multi_mode, seed):
     """Filters of one (m, k) probed as interleaved groups (vbf_multi_part.hip): groups of 3 and of
-    10 (split 8 + 2), mixed with filters of other sizes and an empty-range SST, with and without
-    key ranges; bit-exact against the oracle and against the one-lane-per-key path."""
+    10 (split 8 + 2), pairs at k = 14 and 7, mixed with filters of other sizes and an empty-range SST,
+    with and without key ranges; bit-exact against the oracle and against the one-lane-per-key path."""
     from velarixdb_amd.key_range import SstRange, candidates, contains_all
     rng = np.random.default_rng(seed)
-    specs = [(0.01, 4000)] * 3 + [(1e-4, 2500)] * 10 + [(0.05, 700), (0.001, 3000)]
+    # k = 9 (class 12), 19 (the group pipeline), 14 (class 16) and 7 (class 8) in groups: the interleaved
+    # round-3 pack takes the runtime-k class kernels over 2^17-position segments (round 6)
+    specs = ([(0.01, 4000)] * 3 + [(1e-4, 2500)] * 10 + [(0.05, 700), (0.001, 3000)] + [(1e-3, 3500)] * 2
+             + [(0.03, 3000)] * 2)
     order = rng.permutation(len(specs))
     filters, orc, ranges = [], [], []
     for i in order:

@@ -10,7 +10,10 @@ per-phase hipEvent timings: 0 = full build, 1 = hash + count + scan (no place/co
 2 = hash only (no LDS count either), 3 = seg_or loads without ds_or, 4 = seg_or ds_or on
 synthetic indices without tile loads,
 5 = seg_or without its tile loop (word load + LDS init + write-back), 6 = also without the word
-load, 7 = LDS init only."""
+load, 7 = LDS init only, 8 = k_tile_pack without key loads and SipHash (bit indices from a
+multiply mix of the key number and seed: the count, scan, placement and copy-out alone), 9 = 8
+without the placement and copy-out (the launch's fixed cost: counters, scan, tile loop).
+Round 6 (VERDICT r05 #6): modes 0 / 1 / 8 / 9 split k_tile_pack's non-hash time by cause."""
 import json
 import os
 import subprocess
@@ -41,7 +44,7 @@ print(json.dumps({p: round(ms / max(c, 1), 3) for p, (ms, c) in ph.items() if c}
 """
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for a in (sys.argv[1:] or ["0", "1", "2", "3", "4", "5", "6", "7"]):
+for a in (sys.argv[1:] or ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9"]):
     lib = os.path.join(root, "velarixdb_amd", "libvbf_ablate.so")  # build.py --ablation
     if not os.path.exists(lib):
         sys.exit("missing %s: run `python velarixdb_amd/build.py --ablation` first" % lib)

@@ -130,26 +130,36 @@ hipError_t launch_probe_pack_class_c(int fmt, uint32_t kc, const DevKeys& dk, co
 hipError_t launch_probe_pack_class_d(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
                                      uint32_t* tiles, uint16_t* ends, hipStream_t s);
 
-// One class kernel: m <= 2^31 takes the one-word remainder, above it the general one.
-template <int FMT, bool LP, int KC>
+// The same classes over 2^17-position segments (the multi-SST probe's interleaved filters,
+// vbf_multi_part.hip: m <= 2^28 positions), keys with the length prefix: _a17 (5, 8, 12), _b17 (16,
+// 21, 24, 32) -- round 6: the multi-SST pack at k outside {10, 19} no longer keeps a scratch stash.
+hipError_t launch_probe_pack_class_a17(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
+                                       uint32_t* tiles, uint16_t* ends, hipStream_t s);
+hipError_t launch_probe_pack_class_b17(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
+                                       uint32_t* tiles, uint16_t* ends, hipStream_t s);
+
+// One class kernel: m <= 2^31 takes the one-word remainder, above it the general one (2^17-position
+// segments: always m <= 2^28).
+template <int FMT, bool LP, int KC, int SB = kSegBits>
 hipError_t launch_probe_pack_one_class(const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles, uint32_t* tiles,
                                        uint16_t* ends, hipStream_t s) {
-    auto fn = pl.m <= (1ull << 31) ? k_probe_pack<FMT, LP, 0, true, kSegBits, false, KC>
-                                   : k_probe_pack<FMT, LP, 0, false, kSegBits, false, KC>;
+    auto fn = SB != kSegBits || pl.m <= (1ull << 31) ? k_probe_pack<FMT, LP, 0, true, SB, false, KC>
+                                                     : k_probe_pack<FMT, LP, 0, false, SB, false, KC>;
     hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)pl.lds1);
     if (err == hipSuccess) hipLaunchKernelGGL(fn, dim3(ntiles), dim3(kPBlock), pl.lds1, s, dk, pl, tiles, ends);
     return err;
 }
 
-template <bool LPC, int... KCs>
+template <bool LPC, int SB, int... KCs>
 hipError_t launch_probe_pack_classes(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
                                      uint32_t* tiles, uint16_t* ends, hipStream_t s) {
     hipError_t err = hipErrorNotSupported;
     with_fmt(fmt, LPC, [&]<int FMT, bool LP>() {
         if constexpr (LP == LPC)
-            ((kc == (uint32_t)KCs ? (void)(err = launch_probe_pack_one_class<FMT, LP, KCs>(dk, pl, ntiles, tiles, ends, s))
-                                  : (void)0),
+            ((kc == (uint32_t)KCs
+                  ? (void)(err = launch_probe_pack_one_class<FMT, LP, KCs, SB>(dk, pl, ntiles, tiles, ends, s))
+                  : (void)0),
              ...);
     });
     return err;

@@ -493,6 +493,15 @@ static hipError_t launch_probe_pp(const KeyBatch& kb, uint32_t m, uint32_t k, co
     return hipSuccess;
 }
 
+// The runtime-k class a probe pack of k takes (0: a compiled k, k > 32 or VBF_KCLASS=0): over 2^20-bit
+// segments for k outside {4, 10, 19}; over 2^17-position multi-SST segments (keys with the length
+// prefix) for k outside {4, 10, 19} too (round 6).
+uint32_t probe_class(uint32_t k, int sb) {
+    static const int kcls = [] { const char* e = getenv("VBF_KCLASS"); return e ? atoi(e) : 1; }();
+    if (kcls == 0 || k == 4 || k == 10 || k == 19 || (sb != kSegBits && sb != kByteSegBits)) return 0;
+    return tile_pack_class(k);
+}
+
 ProbePlan make_probe_plan(uint32_t m, uint32_t k, int sb) {
     ProbePlan pl{};
     pl.k = k;
@@ -503,7 +512,7 @@ ProbePlan make_probe_plan(uint32_t m, uint32_t k, int sb) {
     pl.nseg_pad = (pl.nseg + 3) & ~3u;
     // k outside {4, 10, 19} on 2^20-bit segments: the runtime-k class kernel's rounds (its stash holds
     // rounds_max(class) rounds of class slots; the scratch-stash kernel runs any round count)
-    const uint32_t kc = (sb == kSegBits && k != 4 && k != 10 && k != 19) ? tile_pack_class(k) : 0u;
+    const uint32_t kc = probe_class(k, sb);
     const uint32_t rmax = (uint32_t)rounds_max((int)(kc ? kc : k));
     const int64_t avail = (int64_t)(kLdsPerCu / 2) - 64 - 4 * (int64_t)pl.nseg_pad;
     const int64_t kt = std::min<int64_t>(std::min<int64_t>((int64_t)rmax * kPBlock, avail / 4 / k), 4096);
@@ -551,11 +560,18 @@ hipError_t launch_probe_pack_fmt(const DevKeys& dk, const ProbePlan& pl, uint32_
              : k == 19 ? k_probe_pack<FMT, LP, 19, S, SB>  // the reference's default p = 1e-4
                        : k_probe_pack<FMT, LP, 0, false, SB>;
     };
+    if constexpr (SB == kByteSegBits && LP) {
+        // the multi-SST probe's interleaved filters (2^17-position segments): the class kernels
+        // too (round 6; make_probe_plan sizes the tile by the class)
+        const uint32_t kc = probe_class(k, SB);
+        if (kc)
+            return kc <= 12 ? launch_probe_pack_class_a17(FMT, kc, dk, pl, ntiles, tiles, ends, s)
+                            : launch_probe_pack_class_b17(FMT, kc, dk, pl, ntiles, tiles, ends, s);
+    }
     if constexpr (SB == kSegBits) {
         // k outside the compiled set: the runtime-k class kernels (register stash) -- unless
         // VBF_KCLASS=0 keeps the scratch-stash kernel (A/B)
-        static const int kcls = [] { const char* e = getenv("VBF_KCLASS"); return e ? atoi(e) : 1; }();
-        const uint32_t kc = (k != 4 && k != 10 && k != 19 && kcls != 0) ? tile_pack_class(k) : 0u;
+        const uint32_t kc = probe_class(k, SB);
         if (kc) {
             if constexpr (LP)
                 return kc <= 12 ? launch_probe_pack_class_a(FMT, kc, dk, pl, ntiles, tiles, ends, s)

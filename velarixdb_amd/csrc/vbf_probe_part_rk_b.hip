@@ -1,10 +1,14 @@
 // vbf_probe_part_rk_b.hip -- the partitioned probe's runtime-k class packs, classes 16, 21, 24, 32, keys with the length prefix
-// (vbf_probe_pack.hpp).
+// (vbf_probe_pack.hpp), over 2^20-bit filter segments and 2^17-position multi-SST segments.
 #include "vbf_probe_pack.hpp"
 
 namespace vbf {
 hipError_t launch_probe_pack_class_b(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
                                      uint32_t* tiles, uint16_t* ends, hipStream_t s) {
-    return launch_probe_pack_classes<true, 16, 21, 24, 32>(fmt, kc, dk, pl, ntiles, tiles, ends, s);
+    return launch_probe_pack_classes<true, kSegBits, 16, 21, 24, 32>(fmt, kc, dk, pl, ntiles, tiles, ends, s);
+}
+hipError_t launch_probe_pack_class_b17(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
+                                       uint32_t* tiles, uint16_t* ends, hipStream_t s) {
+    return launch_probe_pack_classes<true, kByteSegBits, 16, 21, 24, 32>(fmt, kc, dk, pl, ntiles, tiles, ends, s);
 }
 }  // namespace vbf

@@ -5,6 +5,6 @@
 namespace vbf {
 hipError_t launch_probe_pack_class_c(int fmt, uint32_t kc, const DevKeys& dk, const ProbePlan& pl, uint32_t ntiles,
                                      uint32_t* tiles, uint16_t* ends, hipStream_t s) {
-    return launch_probe_pack_classes<false, 5, 8, 12>(fmt, kc, dk, pl, ntiles, tiles, ends, s);
+    return launch_probe_pack_classes<false, kSegBits, 5, 8, 12>(fmt, kc, dk, pl, ntiles, tiles, ends, s);
 }
 }  // namespace vbf

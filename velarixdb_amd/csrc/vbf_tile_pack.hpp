@@ -277,8 +277,11 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
             const uint32_t slot = (uint32_t)r * kKeysPerRound + tid / SPL;
             const uint32_t seed0 = (uint32_t)KL * (tid % SPL);
             const bool valid = (uint32_t)r < pl.R && slot < nk;
+            // ablation builds only (VBF_ABLATE = 8 / 9, timing experiments): no key loads, no SipHash
+            const bool nohash = VBF_ABLATION_BUILD && (pl.ablate == 8 || pl.ablate == 9);
             Prefix p{};
-            if constexpr (PF) {
+            if (nohash) {
+            } else if constexpr (PF) {
                 const KeyHead h = head_cur;
                 if constexpr (r + 1 < RM) head_cur = head_of(r + 1);
                 if (valid) p = key_prefix_head<LP>(h);
@@ -303,7 +306,9 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
                 uint32_t idx = kSentinel;
                 // class kernels: seeds past the runtime k (wave-uniform) leave sentinels
                 if (valid && (SPL == 1 || seed0 + i < (uint32_t)K) && (KC == 0 || (uint32_t)i < pl.k)) {
-                    const uint64_t h = FMT > 0 ? seed_hash(q, seed0 + i) : prefix_hash(p, seed0 + i);
+                    const uint64_t h =
+                        nohash ? (key0 + slot) * 0x9E3779B97F4A7C15ull ^ (uint64_t)(seed0 + i + 1) * 0xC2B2AE3D27D4EB4Full
+                        : FMT > 0 ? seed_hash(q, seed0 + i) : prefix_hash(p, seed0 + i);
                     idx = mod_m<M31, SAT>(h, pl.m, pl.mu);
                     seg_count<C16, SB>(cnt0, idx);
                 }
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
     // until the hashing rounds ended
     for (uint32_t g = tid; g < (POS == 1 ? pl.CPg : pl.CP) / 8; g += BS) smem[g * kGroupWords + 4] = 0;
     __syncthreads();
-    if (pl.ablate == 1 || pl.ablate == 2) {  // timing experiment: keep the stash live, skip the sort
+    if (pl.ablate == 1 || pl.ablate == 2 || (VBF_ABLATION_BUILD && pl.ablate == 9)) {  // timing experiment: keep the stash live, skip the sort
         uint32_t acc = 0;
         for (uint32_t t = 0; t < ns; ++t) acc ^= stash[t];
         if (acc == 0x12345678u) ends[blockIdx.x] = (uint16_t)acc;
