@@ -54,6 +54,8 @@ for s in $STEPS; do
     benchnostagger) run bench_nostagger 300 env VBF_STAGGER=0 python bench.py --no-cpu-baseline ;;
     benchstagger14) run bench_stagger14 300 env VBF_STAGGER=14 python bench.py --no-cpu-baseline ;;
     ablate) run ablate 300 python tools/ablate.py ;;
+    ablate19) run ablate19 300 env ABL_M=1900000000 ABL_K=19 python tools/ablate.py 0 1 2 3 5 8 9 ;;
+    rdg6)   run rdg6 300 ./tools/rdg6 ;;
     ubhash) run ubench_hash 300 ./tools/ubench hash ;;
     overlap) run overlap 300 ./tools/overlap ;;
     pmcicache) (cd /tmp && run pmcicache 600 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmcicache" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) || exit $? ;;

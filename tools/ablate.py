@@ -34,10 +34,10 @@ words = torch.zeros((m + 31) // 32, dtype=torch.int32, device=dev)
 def run():
     call("vbf_build_dev_ex", ctypes.c_void_p(keys.data_ptr()), None, L, n, 1, m, k,
          ctypes.c_void_p(words.data_ptr()), 2, sp)
-for _ in range(2): run()
+for _ in range(10): run()  # clocks up before the timed launches
 torch.cuda.synchronize()
 lib.vbf_profile_enable(1); profile_read()
-for _ in range(5): run()
+for _ in range(30): run()
 torch.cuda.synchronize()
 ph = profile_read()
 print(json.dumps({p: round(ms / max(c, 1), 3) for p, (ms, c) in ph.items() if c}))

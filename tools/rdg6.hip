@@ -1,0 +1,252 @@
+// rdg6.hip -- k_seg_or's flattened reader (VBF_K3 10/11, vbf_partition.hip) on two packed image
+// formats, to price a format change before building it:
+//   g8 : the current 8-entry groups of 20 B (16 B of u16 low halves, then the group's nibble word):
+//        two load instructions per group (dwordx4 + dword)
+//   g6 : 6-entry groups of 16 B (entry c at bits 20c .. 20c + 19 of the 128-bit group, 8 bits spare):
+//        one dwordx4 per group, 6.7 % more image bytes
+// Run lengths per (tile, segment): mean M, uniform in [M/2, 3M/2] (the real ones are ~Poisson(M)).
+// With OR = 1 every entry is ORed into the segment's 128 KiB LDS bitmap (as k_seg_or); OR = 0 reads
+// only.  One 1024-thread workgroup per segment, XCD-aware segment order, as k_seg_or.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++20 -o tools/rdg6 tools/rdg6.hip
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+__device__ __host__ inline uint32_t mix(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+// run bounds (begin | end << 16, entries) into bnd[seg][tile]; used = max entries per tile
+__global__ void k_gen(uint32_t* bnd, uint32_t ntiles, uint32_t nseg, uint32_t mean, uint32_t* used) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    uint32_t e = 0;
+    for (uint32_t s = 0; s < nseg; ++s) {
+        const uint32_t len = mean / 2 + mix(t * 7919u + s * 104729u + 17u) % (mean + 1);
+        bnd[(uint64_t)s * ntiles + t] = e | ((e + len) << 16);
+        e += len;
+    }
+    atomicMax(used, e);
+}
+
+// random 20-bit entries in either format
+__global__ void k_fill(uint32_t* img, uint64_t words) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < words) img[i] = mix((uint32_t)i * 2654435761u + 12345u) ^ mix((uint32_t)(i >> 32) + 77u);
+}
+
+template <int F> struct Fmt;
+template <> struct Fmt<0> {  // g8
+    static constexpr uint32_t E = 8, GB = 20;
+    __device__ static uint32_t gidx(uint32_t e) { return e >> 3; }
+    __device__ static uint32_t gend(uint32_t e) { return (e + 7) >> 3; }
+};
+template <> struct Fmt<1> {  // g6
+    static constexpr uint32_t E = 6, GB = 16;
+    __device__ static uint32_t gidx(uint32_t e) { return e / 6; }
+    __device__ static uint32_t gend(uint32_t e) { return (e + 5) / 6; }
+};
+
+struct G {
+    uint4 l;
+    uint32_t nib;
+};
+
+template <int F>
+__device__ __forceinline__ void load_g(const uint8_t* tile, uint32_t gi, G& g) {
+    if constexpr (F == 0) {
+        __builtin_memcpy(&g.l, tile + gi * 20, 16);
+        g.nib = *reinterpret_cast<const uint32_t*>(tile + gi * 20 + 16);
+    } else {
+        g.l = *reinterpret_cast<const uint4*>(tile + gi * 16);
+        g.nib = 0;
+    }
+}
+
+template <int F, bool OR>
+__device__ __forceinline__ void or_g(uint32_t* bitmap, const G& g, uint32_t a, uint32_t b, uint32_t& acc) {
+    const uint32_t w[4] = {g.l.x, g.l.y, g.l.z, g.l.w};
+#pragma unroll
+    for (int c = 0; c < (int)Fmt<F>::E; ++c) {
+        if ((uint32_t)c >= a && (uint32_t)c < b) {
+            uint32_t idx;
+            if constexpr (F == 0) {
+                idx = ((w[c >> 1] >> ((c & 1) * 16)) & 0xFFFFu) | (((g.nib >> (4 * c)) & 15u) << 16);
+            } else {
+                const int bit = 20 * c, wi = bit >> 5, sh = bit & 31;
+                if (sh + 20 <= 32)
+                    idx = (w[wi] >> sh) & 0xFFFFFu;
+                else
+                    idx = __builtin_amdgcn_alignbit(w[wi + 1], w[wi], sh) & 0xFFFFFu;
+            }
+            if constexpr (OR)
+                atomicOr(&bitmap[idx >> 5], 1u << (idx & 31));
+            else
+                acc ^= idx;
+        }
+    }
+}
+
+template <int F, bool OR, int NG>
+__global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles,
+                                               uint32_t nseg, uint32_t tile_bytes, uint32_t* out) {
+    __shared__ __attribute__((aligned(16))) uint32_t bitmap[32768];
+    const uint32_t nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
+    const uint32_t seg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t w = tid * 4; w < 32768; w += 4096) *reinterpret_cast<uint4*>(bitmap + w) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    const uint32_t* row = bnd + (uint64_t)seg * ntiles;
+    uint32_t acc = 0;
+    using FM = Fmt<F>;
+    struct FB {
+        uint32_t v, excl, total;
+        G g[NG];
+        uint32_t ab[NG];
+    };
+    auto lb = [&](uint32_t t0) -> uint32_t { return t0 + lane < ntiles ? row[t0 + lane] : 0u; };
+    auto prep = [&](uint32_t v, FB& b) {
+        const uint32_t st = v & 0xFFFFu, en = v >> 16;
+        const uint32_t ch = en > st ? FM::gend(en) - FM::gidx(st) : 0u;
+        uint32_t incl = ch;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= (uint32_t)o) incl += y;
+        }
+        b.v = v;
+        b.excl = incl - ch;
+        b.total = (uint32_t)__shfl((int)incl, 63);
+    };
+    auto locate = [&](const FB& b, uint32_t t0, uint32_t c, const uint8_t*& tile, uint32_t& gi) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int sft = 32; sft; sft >>= 1)
+            if ((uint32_t)__shfl((int)b.excl, (int)r + sft) <= c) r += sft;
+        const uint32_t rv = (uint32_t)__shfl((int)b.v, (int)r), rex = (uint32_t)__shfl((int)b.excl, (int)r);
+        const uint32_t rst = rv & 0xFFFFu, ren = rv >> 16;
+        tile = img + (uint64_t)min(t0 + r, ntiles - 1) * tile_bytes;
+        gi = FM::gidx(rst) + (c - rex);
+        if (c >= b.total) return 0u;
+        const uint32_t g0 = gi * FM::E;
+        const uint32_t a = g0 < rst ? rst - g0 : 0u, e = min(FM::E, ren - g0);
+        return a | (e << 4);
+    };
+    auto issue = [&](uint32_t t0, FB& b) {
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            const uint8_t* tile;
+            uint32_t gi;
+            b.ab[q] = locate(b, t0, (uint32_t)q * 64 + lane, tile, gi);
+            if (b.ab[q]) load_g<F>(tile, gi, b.g[q]);
+        }
+    };
+    auto consume = [&](uint32_t t0, const FB& b) {
+#pragma unroll
+        for (int q = 0; q < NG; ++q)
+            if (b.ab[q]) or_g<F, OR>(bitmap, b.g[q], b.ab[q] & 15u, b.ab[q] >> 4, acc);
+#pragma unroll 1
+        for (uint32_t c0 = 64 * NG; c0 < b.total; c0 += 64) {
+            const uint8_t* tile;
+            uint32_t gi;
+            const uint32_t ab = locate(b, t0, c0 + lane, tile, gi);
+            if (ab) {
+                G g;
+                load_g<F>(tile, gi, g);
+                or_g<F, OR>(bitmap, g, ab & 15u, ab >> 4, acc);
+            }
+        }
+    };
+    const uint32_t wstep = 16 * 64;
+    uint32_t t0 = wave * 64;
+    FB A, B;
+    uint32_t v1 = lb(t0 + wstep);
+    prep(lb(t0), A);
+    if (t0 < ntiles) issue(t0, A);
+    while (t0 < ntiles) {
+        prep(v1, B);
+        uint32_t v2 = lb(t0 + 2 * wstep);
+        const bool more = t0 + wstep < ntiles;
+        if (more) issue(t0 + wstep, B);
+        consume(t0, A);
+        t0 += wstep;
+        if (!more) break;
+        prep(v2, A);
+        v1 = lb(t0 + 2 * wstep);
+        const bool more2 = t0 + wstep < ntiles;
+        if (more2) issue(t0 + wstep, A);
+        consume(t0, B);
+        t0 += wstep;
+        if (!more2) break;
+    }
+    __syncthreads();
+    uint32_t x = acc;
+    for (uint32_t w = tid; w < 32768; w += 1024) x ^= bitmap[w];
+    if (x == 0x12345678u) out[seg] = x;
+}
+
+template <int F, bool OR, int NG>
+static float run(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles, uint32_t nseg, uint32_t tile_bytes,
+                 uint32_t* out) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int r = 0; r < 3; ++r)
+        hipLaunchKernelGGL((k_read<F, OR, NG>), dim3(nseg), dim3(1024), 0, 0, img, bnd, ntiles, nseg, tile_bytes, out);
+    (void)hipEventRecord(e0);
+    for (int r = 0; r < 20; ++r)
+        hipLaunchKernelGGL((k_read<F, OR, NG>), dim3(nseg), dim3(1024), 0, 0, img, bnd, ntiles, nseg, tile_bytes, out);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    return ms / 20;
+}
+
+int main() {
+    struct Cfg { const char* name; uint32_t ntiles, nseg, mean; };
+    // k = 10: 100M keys / 3072 per tile, m = 1e9 (954 segments); k = 19: 100M / 1536, m = 1.9e9;
+    // config 5: 1B keys / 7168 per tile, k = 4, 4096 segments (~7-entry runs)
+    const Cfg cfgs[] = {{"k10", 32553, 954, 32}, {"k19", 65105, 1812, 16}, {"cfg5", 139509, 4096, 7}};
+    for (const Cfg& c : cfgs) {
+        uint32_t *bnd, *used, *out;
+        const uint64_t nb = (uint64_t)c.ntiles * c.nseg;
+        if (hipMalloc(&bnd, nb * 4) != hipSuccess || hipMalloc(&used, 4) != hipSuccess ||
+            hipMalloc(&out, 4 * 4096) != hipSuccess)
+            return 1;
+        (void)hipMemset(used, 0, 4);
+        hipLaunchKernelGGL(k_gen, dim3((c.ntiles + 255) / 256), dim3(256), 0, 0, bnd, c.ntiles, c.nseg, c.mean, used);
+        uint32_t cap = 0;
+        (void)hipMemcpy(&cap, used, 4, hipMemcpyDeviceToHost);
+        for (int f = 0; f < 2; ++f) {
+            const uint32_t tile_bytes = f == 0 ? ((cap + 7) / 8 * 20 + 15) / 16 * 16 + 16 : ((cap + 5) / 6) * 16 + 16;
+            const uint64_t bytes = (uint64_t)c.ntiles * tile_bytes + 4096;
+            uint8_t* img;
+            if (hipMalloc(&img, bytes) != hipSuccess) return 1;
+            hipLaunchKernelGGL(k_fill, dim3((unsigned)((bytes / 4 + 255) / 256)), dim3(256), 0, 0,
+                               reinterpret_cast<uint32_t*>(img), bytes / 4);
+            auto show = [&](const char* v, float ms) {
+                printf("%s %s %-10s %.3f ms  (%.1f G runs/s, %u B per tile, %.2f GB image)\n", c.name,
+                       f ? "g6" : "g8", v, ms, (double)nb / (ms * 1e-3) / 1e9, tile_bytes,
+                       (double)c.ntiles * tile_bytes / 1e9);
+                fflush(stdout);
+            };
+            if (f == 0) {
+                show("read ng4", run<0, false, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("or ng4", run<0, true, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("or ng5", run<0, true, 5>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+            } else {
+                show("read ng4", run<1, false, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("or ng4", run<1, true, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("or ng5", run<1, true, 5>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("or ng6", run<1, true, 6>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+            }
+            (void)hipFree(img);
+        }
+        (void)hipFree(bnd);
+        (void)hipFree(used);
+        (void)hipFree(out);
+    }
+    return 0;
+}
