@@ -48,6 +48,12 @@ template <> struct Fmt<1> {  // g6
     __device__ static uint32_t gend(uint32_t e) { return (e + 5) / 6; }
 };
 
+template <> struct Fmt<2> {  // c8: the g8 image, a run read as the 16-byte chunks its groups span
+    static constexpr uint32_t E = 8, GB = 20;
+    __device__ static uint32_t gidx(uint32_t e) { return 5 * (e >> 3) / 4; }
+    __device__ static uint32_t gend(uint32_t e) { return (5 * ((e + 7) >> 3) + 3) / 4; }
+};
+
 struct G {
     uint4 l;
     uint32_t nib;
@@ -61,6 +67,34 @@ __device__ __forceinline__ void load_g(const uint8_t* tile, uint32_t gi, G& g) {
     } else {
         g.l = *reinterpret_cast<const uint4*>(tile + gi * 16);
         g.nib = 0;
+    }
+}
+
+// c8: chunk cj of the run [st, en) (words 4cj .. 4cj + 3 in l), the next chunk in n
+template <bool OR>
+__device__ __forceinline__ void or_chunk(uint32_t* bitmap, uint4 l, uint4 n, uint32_t cj, uint32_t st, uint32_t en,
+                                         uint32_t& acc) {
+    const uint32_t X[8] = {l.x, l.y, l.z, l.w, n.x, n.y, n.z, n.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t w = 4 * cj + i, g = w / 5, r = w - 5 * g;
+        if (r == 4) continue;
+        const uint32_t li = i + 4 - r;  // the group's nibble word: X[i + 1 .. i + 4]
+        uint32_t nib = X[i + 1];
+#pragma unroll
+        for (int d = 2; d <= 4; ++d)
+            if (li == (uint32_t)(i + d)) nib = X[i + d];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t e = 8 * g + 2 * r + h;
+            if (e >= st && e < en) {
+                const uint32_t idx = ((X[i] >> (16 * h)) & 0xFFFFu) | (((nib >> (8 * r + 4 * h)) & 15u) << 16);
+                if constexpr (OR)
+                    atomicOr(&bitmap[idx >> 5], 1u << (idx & 31));
+                else
+                    acc ^= idx;
+            }
+        }
     }
 }
 
@@ -105,6 +139,66 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
         G g[NG];
         uint32_t ab[NG];
     };
+    if constexpr (F == 2) {
+        // flattened chunks: lane c of a batch reads chunk (c - excl(run)) of its run; the next chunk
+        // of the same run comes from lane c + 1 (lane 63 loads it itself)
+        auto lb2 = [&](uint32_t t0) -> uint32_t { return t0 + lane < ntiles ? row[t0 + lane] : 0u; };
+        const uint32_t wstep = 16 * 64;
+        for (uint32_t t0 = wave * 64; t0 < ntiles; t0 += wstep) {
+            FB b;
+            const uint32_t v = lb2(t0);
+            {
+                const uint32_t st = v & 0xFFFFu, en = v >> 16;
+                const uint32_t ch = en > st ? FM::gend(en) - FM::gidx(st) : 0u;
+                uint32_t incl = ch;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o);
+                    if (lane >= (uint32_t)o) incl += y;
+                }
+                b.v = v;
+                b.excl = incl - ch;
+                b.total = (uint32_t)__shfl((int)incl, 63);
+            }
+            for (uint32_t c0 = 0; c0 < b.total; c0 += 64 * NG) {
+                uint4 L[NG];
+                uint32_t cj[NG], rst[NG], ren[NG], last[NG];
+                const uint8_t* tl[NG];
+#pragma unroll
+                for (int q = 0; q < NG; ++q) {
+                    const uint32_t c = c0 + q * 64 + lane;
+                    uint32_t r = 0;
+#pragma unroll
+                    for (int sft = 32; sft; sft >>= 1)
+                        if ((uint32_t)__shfl((int)b.excl, (int)r + sft) <= c) r += sft;
+                    const uint32_t rv = (uint32_t)__shfl((int)b.v, (int)r), rex = (uint32_t)__shfl((int)b.excl, (int)r);
+                    rst[q] = rv & 0xFFFFu;
+                    ren[q] = rv >> 16;
+                    tl[q] = img + (uint64_t)min(t0 + r, ntiles - 1) * tile_bytes;
+                    cj[q] = FM::gidx(rst[q]) + (c - rex);
+                    last[q] = cj[q] + 1 >= FM::gend(ren[q]);
+                    if (c >= b.total) ren[q] = 0;  // no entries
+                    if (ren[q]) L[q] = *reinterpret_cast<const uint4*>(tl[q] + cj[q] * 16);
+                    else L[q] = make_uint4(0, 0, 0, 0);
+                }
+#pragma unroll
+                for (int q = 0; q < NG; ++q) {
+                    uint4 N;
+                    N.x = (uint32_t)__shfl_down((int)L[q].x, 1);
+                    N.y = (uint32_t)__shfl_down((int)L[q].y, 1);
+                    N.z = (uint32_t)__shfl_down((int)L[q].z, 1);
+                    N.w = (uint32_t)__shfl_down((int)L[q].w, 1);
+                    if (lane == 63 && ren[q] && !last[q]) N = *reinterpret_cast<const uint4*>(tl[q] + cj[q] * 16 + 16);
+                    if (ren[q]) {
+                        if constexpr (OR)
+                            or_chunk<true>(bitmap, L[q], N, cj[q], rst[q], ren[q], acc);
+                        else
+                            acc ^= L[q].x ^ L[q].y ^ L[q].z ^ L[q].w ^ N.x;
+                    }
+                }
+            }
+        }
+    } else {
     auto lb = [&](uint32_t t0) -> uint32_t { return t0 + lane < ntiles ? row[t0 + lane] : 0u; };
     auto prep = [&](uint32_t v, FB& b) {
         const uint32_t st = v & 0xFFFFu, en = v >> 16;
@@ -129,6 +223,7 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
         tile = img + (uint64_t)min(t0 + r, ntiles - 1) * tile_bytes;
         gi = FM::gidx(rst) + (c - rex);
         if (c >= b.total) return 0u;
+        if constexpr (F == 2) return 1u;
         const uint32_t g0 = gi * FM::E;
         const uint32_t a = g0 < rst ? rst - g0 : 0u, e = min(FM::E, ren - g0);
         return a | (e << 4);
@@ -180,10 +275,19 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
         t0 += wstep;
         if (!more2) break;
     }
+    }
     __syncthreads();
     uint32_t x = acc;
-    for (uint32_t w = tid; w < 32768; w += 1024) x ^= bitmap[w];
-    if (x == 0x12345678u) out[seg] = x;
+    for (uint32_t w = tid; w < 32768; w += 1024) x ^= bitmap[w] * (w * 2654435761u + 1u);
+    for (int o = 32; o > 0; o >>= 1) x ^= (uint32_t)__shfl_down((int)x, o);
+    __shared__ uint32_t wx[16];
+    if (lane == 0) wx[wave] = x;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t y = 0;
+        for (int i = 0; i < 16; ++i) y ^= wx[i];
+        out[seg] = y;  // a checksum of the segment's bitmap (OR runs of one image agree)
+    }
 }
 
 template <int F, bool OR, int NG>
@@ -227,15 +331,22 @@ int main() {
             hipLaunchKernelGGL(k_fill, dim3((unsigned)((bytes / 4 + 255) / 256)), dim3(256), 0, 0,
                                reinterpret_cast<uint32_t*>(img), bytes / 4);
             auto show = [&](const char* v, float ms) {
-                printf("%s %s %-10s %.3f ms  (%.1f G runs/s, %u B per tile, %.2f GB image)\n", c.name,
+                static uint32_t h[4096];
+                (void)hipMemcpy(h, out, 4 * c.nseg, hipMemcpyDeviceToHost);
+                uint64_t sum = 0;
+                for (uint32_t i = 0; i < c.nseg; ++i) sum = sum * 1000003u + h[i];
+                printf("%s %s %-12s %.3f ms  (%.1f G runs/s, %u B per tile, %.2f GB image) check %016llx\n", c.name,
                        f ? "g6" : "g8", v, ms, (double)nb / (ms * 1e-3) / 1e9, tile_bytes,
-                       (double)c.ntiles * tile_bytes / 1e9);
+                       (double)c.ntiles * tile_bytes / 1e9, (unsigned long long)sum);
                 fflush(stdout);
             };
             if (f == 0) {
                 show("read ng4", run<0, false, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
                 show("or ng4", run<0, true, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
                 show("or ng5", run<0, true, 5>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("c8 read ng4", run<2, false, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("c8 or ng4", run<2, true, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("c8 or ng6", run<2, true, 6>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
             } else {
                 show("read ng4", run<1, false, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
                 show("or ng4", run<1, true, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
