@@ -506,7 +506,8 @@ def test_partitioned_build_knobs_same_words(vbf, ora, tmp_path):
     """The speed-only knobs of the fixed-length partitioned build -- VBF_K1 (the 1024-thread K1 with
     two lanes per key at k = 19, or the 512-thread one-lane-per-key shape), VBF_ENDS_T (K1 writes
     the run ends transposed, or the transpose kernel does), VBF_K3 (k_seg_or's tile loops: two-stage,
-    three-stage with 8-lane groups and its >8-group tail, flattened groups) -- must give the
+    three-stage with 8-lane groups and its >8-group tail, flattened groups found by binary search or,
+    the default since round 6, by run marks) -- must give the
     oracle's words in every combination, on random keys and on a batch whose runs are thousands of
     entries long (three keys repeated).  Each combination builds in a child process (the library
     reads the knobs once per process)."""
@@ -542,7 +543,8 @@ def test_partitioned_build_knobs_same_words(vbf, ora, tmp_path):
     # (VBF_K1, VBF_ENDS_T, VBF_K3, VBF_K3_SPLIT): the last one splits k_seg_or's last round of
     # segments over several workgroups (m = 2_999_999_999: 2 862 segments)
     combos = (("0", "0", "0", "1"), ("1", "1", "0", "0"), ("1", "0", "3", "1"), ("0", "1", "1", "1"),
-              ("1", "1", "4", "1"), ("-1", "1", "12", "0"), ("0", "0", "10", "1"), ("1", "1", "13", "1"))
+              ("1", "1", "4", "1"), ("-1", "1", "12", "0"), ("0", "0", "10", "1"), ("1", "1", "13", "1"),
+              ("1", "1", "16", "0"), ("0", "1", "11", "1"))
     for k1, et, k3, sp in combos:
         env = {kk: vv for kk, vv in os.environ.items() if kk != "VBF_LIB"}
         env["VBF_K1"], env["VBF_ENDS_T"], env["VBF_K3"], env["VBF_K3_SPLIT"] = k1, et, k3, sp

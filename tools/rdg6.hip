@@ -36,6 +36,26 @@ __global__ void k_fill(uint32_t* img, uint64_t words) {
     if (i < words) img[i] = mix((uint32_t)i * 2654435761u + 12345u) ^ mix((uint32_t)(i >> 32) + 77u);
 }
 
+// inclusive sum / max over the lanes of a wave with DPP row shifts and row broadcasts (no LDS)
+__device__ __forceinline__ uint32_t scan_add(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
+__device__ __forceinline__ uint32_t scan_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+    return x;
+}
+
 template <int F> struct Fmt;
 template <> struct Fmt<0> {  // g8
     static constexpr uint32_t E = 8, GB = 20;
@@ -122,10 +142,15 @@ __device__ __forceinline__ void or_g(uint32_t* bitmap, const G& g, uint32_t a, u
     }
 }
 
-template <int F, bool OR, int NG>
+// LOC = 0: a group finds its run by a 6-step binary search over the wave's group prefix (ds_bpermute,
+// as k_seg_or); LOC = 1: the prefix by a DPP scan, and each run marks its first group in a per-wave
+// LDS byte table -- a group's run is the DPP max-scan of the marks, its bounds one ds_read_b64.
+template <int F, bool OR, int NG, int LOC = 0>
 __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles,
                                                uint32_t nseg, uint32_t tile_bytes, uint32_t* out) {
     __shared__ __attribute__((aligned(16))) uint32_t bitmap[32768];
+    __shared__ __attribute__((aligned(16))) uint32_t marks_w[16][LOC ? NG * 16 : 1];
+    __shared__ __attribute__((aligned(16))) uint2 info[16][LOC ? 64 : 1];
     const uint32_t nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
     const uint32_t seg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + blockIdx.x / 8;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -204,14 +229,19 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
         const uint32_t st = v & 0xFFFFu, en = v >> 16;
         const uint32_t ch = en > st ? FM::gend(en) - FM::gidx(st) : 0u;
         uint32_t incl = ch;
+        if constexpr (LOC == 1) {
+            incl = scan_add(ch);
+            b.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        } else {
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= (uint32_t)o) incl += y;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= (uint32_t)o) incl += y;
+            }
+            b.total = (uint32_t)__shfl((int)incl, 63);
         }
         b.v = v;
         b.excl = incl - ch;
-        b.total = (uint32_t)__shfl((int)incl, 63);
     };
     auto locate = [&](const FB& b, uint32_t t0, uint32_t c, const uint8_t*& tile, uint32_t& gi) -> uint32_t {
         uint32_t r = 0;
@@ -229,12 +259,42 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
         return a | (e << 4);
     };
     auto issue = [&](uint32_t t0, FB& b) {
+        if constexpr (LOC == 1) {
+            uint8_t* mk = reinterpret_cast<uint8_t*>(marks_w[wave]);
+            for (uint32_t w = lane; w < NG * 16; w += 64) marks_w[wave][w] = 0;
+            info[wave][lane] = make_uint2(b.v, b.excl);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t st = b.v & 0xFFFFu, en = b.v >> 16;
+            if (en > st && b.excl < 64u * NG) mk[b.excl] = (uint8_t)(lane + 1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            uint32_t carry = 0;
 #pragma unroll
-        for (int q = 0; q < NG; ++q) {
-            const uint8_t* tile;
-            uint32_t gi;
-            b.ab[q] = locate(b, t0, (uint32_t)q * 64 + lane, tile, gi);
-            if (b.ab[q]) load_g<F>(tile, gi, b.g[q]);
+            for (int q = 0; q < NG; ++q) {
+                const uint32_t c = (uint32_t)q * 64 + lane;
+                uint32_t r1 = max(scan_max((uint32_t)mk[c]), carry);
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)r1, 63);
+                b.ab[q] = 0;
+                if (c < b.total) {
+                    const uint2 ri = info[wave][r1 - 1];
+                    const uint32_t rst = ri.x & 0xFFFFu, ren = ri.x >> 16;
+                    const uint8_t* tile = img + (uint64_t)min(t0 + r1 - 1, ntiles - 1) * tile_bytes;
+                    const uint32_t gi = FM::gidx(rst) + (c - ri.y);
+                    const uint32_t g0 = gi * FM::E;
+                    const uint32_t a = g0 < rst ? rst - g0 : 0u, e = min(FM::E, ren - g0);
+                    b.ab[q] = a | (e << 4);
+                    load_g<F>(tile, gi, b.g[q]);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NG; ++q) {
+                const uint8_t* tile;
+                uint32_t gi;
+                b.ab[q] = locate(b, t0, (uint32_t)q * 64 + lane, tile, gi);
+                if (b.ab[q]) load_g<F>(tile, gi, b.g[q]);
+            }
         }
     };
     auto consume = [&](uint32_t t0, const FB& b) {
@@ -290,17 +350,17 @@ __global__ __launch_bounds__(1024) void k_read(const uint8_t* img, const uint32_
     }
 }
 
-template <int F, bool OR, int NG>
+template <int F, bool OR, int NG, int LOC = 0>
 static float run(const uint8_t* img, const uint32_t* bnd, uint32_t ntiles, uint32_t nseg, uint32_t tile_bytes,
                  uint32_t* out) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     for (int r = 0; r < 3; ++r)
-        hipLaunchKernelGGL((k_read<F, OR, NG>), dim3(nseg), dim3(1024), 0, 0, img, bnd, ntiles, nseg, tile_bytes, out);
+        hipLaunchKernelGGL((k_read<F, OR, NG, LOC>), dim3(nseg), dim3(1024), 0, 0, img, bnd, ntiles, nseg, tile_bytes, out);
     (void)hipEventRecord(e0);
     for (int r = 0; r < 20; ++r)
-        hipLaunchKernelGGL((k_read<F, OR, NG>), dim3(nseg), dim3(1024), 0, 0, img, bnd, ntiles, nseg, tile_bytes, out);
+        hipLaunchKernelGGL((k_read<F, OR, NG, LOC>), dim3(nseg), dim3(1024), 0, 0, img, bnd, ntiles, nseg, tile_bytes, out);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms = 0;
@@ -346,7 +406,11 @@ int main() {
                 show("or ng5", run<0, true, 5>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
                 show("c8 read ng4", run<2, false, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
                 show("c8 or ng4", run<2, true, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
-                show("c8 or ng6", run<2, true, 6>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("mk read ng4", run<0, false, 4, 1>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("mk or ng4", run<0, true, 4, 1>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("mk or ng5", run<0, true, 5, 1>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("mk or ng6", run<0, true, 6, 1>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
+                show("or ng4", run<0, true, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
             } else {
                 show("read ng4", run<1, false, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));
                 show("or ng4", run<1, true, 4>(img, bnd, c.ntiles, c.nseg, tile_bytes, out));

@@ -51,8 +51,6 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     """One hipcc per translation unit, in parallel, then one link.  `defines` (e.g.
     VBF_ABLATION_BUILD=1 for tools/ablate.py, written to velarixdb_amd/libvbf_ablate.so) build a
     variant library for VBF_LIB; the product is libvbf.so without any."""
-    if out == OUT and not defines and not force and not needs_build():
-        return OUT
     tag = "_".join(d.replace("=", "") for d in defines)
     objdir = os.path.join(HERE, "..", "build", "obj" + ("_" + tag if tag else ""))
     os.makedirs(objdir, exist_ok=True)
@@ -74,6 +72,11 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     failed = [s for s, p in procs if p.wait() != 0]
     if failed:
         raise RuntimeError("hipcc failed for " + ", ".join(failed))
+    # every object current (against its own sources, so a header edited while an earlier build ran
+    # still recompiles what includes it) and the library newer than all of them: nothing to link
+    if not procs and not force and os.path.exists(out) and \
+            os.path.getmtime(out) > max(os.path.getmtime(o) for o in objs):
+        return out
     cmd = [_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -151,8 +151,8 @@ __device__ __forceinline__ uint32_t group_range(uint32_t gi, uint32_t st, uint32
     return a | (b << 4);
 }
 
-// K3 tile-loop variants (speed only; identical results).  By default the plan picks V3 (NG = 5)
-// for runs of >= kShortRun entries on average (C / nseg) and V6 (NG = 4) below; VBF_K3 forces one:
+// K3 tile-loop variants (speed only; identical results).  By default the plan picks V7 with NG = 5
+// for runs of >= kShortRun entries on average (C / nseg) and NG = 4 below; VBF_K3 forces one:
 //   1: two-stage -- run bounds of batch b+1 (8 u16 loads per lane) in flight with batch b's data
 //   3: three-stage -- bounds of b+2, data of b+1 and the ORs of b overlap; run bounds loaded
 //      coalesced (one u16 pair per lane for the wave's tiles) and handed to the 8-lane groups with
@@ -164,6 +164,8 @@ __device__ __forceinline__ uint32_t group_range(uint32_t gi, uint32_t st, uint32
 //   6: flattened -- a wave's runs' groups dealt to lanes back to back, no lane idles on a short
 //      run (VBF_K3 10: NG=4, 11: NG=5, 12: NG=6).  At k = 19 (m = 1.9e9, ~16-entry runs) it is
 //      the one that keeps K3 from idling most of its lanes.
+//   7: the flattened reader with each group's run found from per-wave run marks in LDS and a DPP
+//      max-scan instead of the binary search (round 6; VBF_K3 14: NG=4, 15: NG=5, 16: NG=6).
 //   Measured and dropped (tools/env_ab.sh): coalesced bounds in the two-stage loop (-3 %);
 //   raw buffer loads with out-of-range offsets for idle lanes (no duplicate requests): the same
 //   as the duplicates (the texture addresser coalesces them).
@@ -172,6 +174,11 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
                                                     uint32_t ntiles, PartPlan pl, bool atomic_merge,
                                                     uint32_t* words) {
     __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
+    // V = 7 (the flattened reader with the run marks, below): per wave, a byte per group slot of the
+    // batch and the batch's 64 run bounds
+    constexpr bool MK = V == 7;
+    __shared__ __attribute__((aligned(16))) uint32_t marks[BS / 64][MK ? NG * 16 : 1];
+    __shared__ __attribute__((aligned(16))) uint2 rinfo[BS / 64][MK ? 64 : 1];
     // XCD-aware order (blocks are dealt round-robin over the 8 XCDs; speed only, never
     // correctness): consecutive segments run on one XCD at the same time, and since a tile
     // stores its segments' runs back to back, they share the L2 lines those short runs sit in.
@@ -247,7 +254,7 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
 
     if (pl.ablate >= 5) {
         // 5-7: timing experiments, fixed costs only
-    } else if constexpr (V == 6) {
+    } else if constexpr (V == 6 || V == 7) {
         // Flattened groups for SHORT runs (large k or m: C / nseg entries per run): the groups of
         // a wave's 64 runs (one per tile, bounds in lane order) are dealt to lanes back to back,
         // so no lane idles on a short run.  A lane finds its run by a 6-step binary search over
@@ -264,14 +271,19 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
             const uint32_t st = v & 0xFFFFu, en = v >> 16;
             const uint32_t ch = en > st ? ((en + 7) >> 3) - (st >> 3) : 0u;
             uint32_t incl = ch;
+            if constexpr (MK) {  // DPP: no LDS instruction
+                incl = wave_incl_scan_dpp(ch);
+                b.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            } else {
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(incl, o);
-                if (lane >= (uint32_t)o) incl += y;
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o);
+                    if (lane >= (uint32_t)o) incl += y;
+                }
+                b.total = (uint32_t)__shfl((int)incl, 63);
             }
             b.v = v;
             b.excl = incl - ch;
-            b.total = (uint32_t)__shfl((int)incl, 63);
         };
         // group c of the batch at t0 -> (tile, group index, live entries a | b << 4; 0 past the end)
         auto locate = [&](const FB& b, uint32_t t0, uint32_t c, const uint32_t*& tile, uint32_t& gi) -> uint32_t {
@@ -286,12 +298,47 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
             return c < b.total ? group_range(gi, rst, ren) : 0u;
         };
         auto issue = [&](uint32_t t0, FB& b) {
+            if constexpr (MK) {
+                // Round 6 (V = 7): the binary search costs 8 ds_bpermute per group -- more LDS
+                // instructions than the group's ORs.  Instead each run writes its bounds to rinfo and
+                // marks its first group slot (run + 1) in a byte table; a slot's run is then the max
+                // of the marks up to it (a DPP scan, carried across the NG slot rows) and its bounds
+                // one ds_read_b64: ~2 LDS instructions per group (tools/rdg6, profiles/r06/rdg6.log:
+                // -14 / -17 / -21 % at k = 10 / 19 / config 5).  Slots past 64 * NG keep the search
+                // (consume).  One wave's LDS operations run in order; the fences keep the compiler's.
+                uint8_t* mk = reinterpret_cast<uint8_t*>(marks[wave]);
+                for (uint32_t w = lane; w < NG * 16; w += 64) marks[wave][w] = 0;
+                rinfo[wave][lane] = make_uint2(b.v, b.excl);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t st = b.v & 0xFFFFu, en = b.v >> 16;
+                if (en > st && b.excl < 64u * NG) mk[b.excl] = (uint8_t)(lane + 1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                uint32_t carry = 0;
 #pragma unroll
-            for (int q = 0; q < NG; ++q) {
-                const uint32_t* tile;
-                uint32_t gi;
-                b.ab[q] = locate(b, t0, (uint32_t)q * 64 + lane, tile, gi);
-                if (b.ab[q]) load_group(tile, gi, b.l[q], b.nib[q]);
+                for (int q = 0; q < NG; ++q) {
+                    const uint32_t c = (uint32_t)q * 64 + lane;
+                    const uint32_t r1 = max(wave_incl_max_dpp((uint32_t)mk[c]), carry);
+                    carry = (uint32_t)__builtin_amdgcn_readlane((int)r1, 63);
+                    b.ab[q] = 0;
+                    if (c < b.total) {  // r1 >= 1: some run starts at or before c
+                        const uint2 ri = rinfo[wave][r1 - 1];
+                        const uint32_t rst = ri.x & 0xFFFFu, ren = ri.x >> 16;
+                        const uint32_t gi = (rst >> 3) + (c - ri.y);
+                        b.ab[q] = group_range(gi, rst, ren);
+                        load_group(tiles + (uint64_t)std::min(t0 + r1 - 1, t_hi - 1) * pl.tile_words, gi, b.l[q],
+                                   b.nib[q]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < NG; ++q) {
+                    const uint32_t* tile;
+                    uint32_t gi;
+                    b.ab[q] = locate(b, t0, (uint32_t)q * 64 + lane, tile, gi);
+                    if (b.ab[q]) load_group(tile, gi, b.l[q], b.nib[q]);
+                }
             }
         };
         auto consume = [&](uint32_t t0, const FB& b) {
@@ -776,9 +823,12 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
         phase_begin(kPhaseSegOr, s);
         // the flattened variant, NG = 4 for short runs (large k or m), 5 otherwise (group layout,
         // profiles/r03/matrix1.log: k = 10 seg_or 1.011 (V3) -> 0.861 ms, k = 19 NG 4 2.26 vs NG 5
-        // 2.34 ms); VBF_K3 overrides
-        const uint32_t k3v = pl.k3v ? pl.k3v : (pl.C / std::max(pl.nseg, 1u) < kShortRun ? 10u : 11u);
-        auto k3 = k3v == 13 ? k_seg_or<3, kPBlock, 4, 4>
+        // 2.34 ms), with the run marks since round 6 (V7); VBF_K3 overrides (10 / 11: round 5's)
+        const uint32_t k3v = pl.k3v ? pl.k3v : (pl.C / std::max(pl.nseg, 1u) < kShortRun ? 14u : 15u);
+        auto k3 = k3v == 14 ? k_seg_or<7, kPBlock, 4>
+                : k3v == 15 ? k_seg_or<7, kPBlock, 5>
+                : k3v == 16 ? k_seg_or<7, kPBlock, 6>
+                : k3v == 13 ? k_seg_or<3, kPBlock, 4, 4>
                 : k3v == 10 ? k_seg_or<6, kPBlock, 4>
                 : k3v == 11 ? k_seg_or<6, kPBlock, 5>
                 : k3v == 12 ? k_seg_or<6, kPBlock, 6>

@@ -81,6 +81,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
     return x;
 }
 
+// Inclusive max over the lanes of a wave, the same DPP pattern (no LDS).
+__device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+    return x;
+}
+
 // Exclusive scan of v[0..n) in LDS (n <= PER * blockDim.x, blockDim.x <= kPBlock).  EVEN: scan the
 // counts rounded up to even (the build's even-length runs) in the same pass.  One barrier: after
 // it every wave adds up the totals of the waves before it itself instead of waiting for one wave

@@ -35,11 +35,15 @@ static hipError_t launch_pu_pack_class(int fmt, const DevKeys& dk, const PartPla
 
 // U3.  Blocks: G consecutive tile ranges per segment, XCD-aware (neighbouring segments on one XCD
 // share the L2 lines their short runs sit in, as in k_seg_or).
-template <int NG = 4>
+// MK: a group's run from per-wave run marks and a DPP max-scan (as k_seg_or V7, vbf_partition.hip)
+// instead of the binary search's ds_bpermutes.
+template <int NG = 4, bool MK = true>
 __global__ __launch_bounds__(kPBlock) void k_probe_seg3(const uint32_t* tiles, const uint32_t* endsT, uint32_t ntiles,
                                                         PartPlan pl, uint32_t G, const uint32_t* words, uint8_t* res,
                                                         uint32_t rstride) {
     __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
+    __shared__ __attribute__((aligned(16))) uint32_t marks[kPBlock / 64][MK ? NG * 16 : 1];
+    __shared__ __attribute__((aligned(16))) uint4 rinfo[kPBlock / 64][MK ? 64 : 1];
     const uint32_t nwg = gridDim.x, qq = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
     const uint32_t wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + blockIdx.x / 8;
     const uint32_t seg = wg / G, part = wg % G;
@@ -96,15 +100,20 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg3(const uint32_t* tiles, c
         const uint32_t st = b & 0xFFFFu, en = e & 0xFFFFu;
         const uint32_t ch = en > st ? ((en + 7) >> 3) - (st >> 3) : 0u;
         uint32_t incl = ch;
+        if constexpr (MK) {
+            incl = wave_incl_scan_dpp(ch);
+            f.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        } else {
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= (uint32_t)o) incl += y;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= (uint32_t)o) incl += y;
+            }
+            f.total = (uint32_t)__shfl((int)incl, 63);
         }
         f.b = b;
         f.e = e;
         f.excl = incl - ch;
-        f.total = (uint32_t)__shfl((int)incl, 63);
     };
     // group c of the batch -> run r (binary search over the exclusive prefix), tile, group index and
     // the group's number j within its run
@@ -142,14 +151,46 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg3(const uint32_t* tiles, c
     };
     const uint32_t wstep = (kPBlock / 64) * 64;
     auto issue = [&](uint32_t t0, FB& f) {
+        if constexpr (MK) {
+            // each run marks its first group slot (run + 1) and leaves its bounds in rinfo; a slot's
+            // run is the max of the marks up to it (slots past 64 * NG: the search, in consume)
+            uint8_t* mk = reinterpret_cast<uint8_t*>(marks[wave]);
+            for (uint32_t w = lane; w < NG * 16; w += 64) marks[wave][w] = 0;
+            rinfo[wave][lane] = make_uint4(f.b, f.e, f.excl, 0u);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if ((f.e & 0xFFFFu) > (f.b & 0xFFFFu) && f.excl < 64u * NG) mk[f.excl] = (uint8_t)(lane + 1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            uint32_t carry = 0;
 #pragma unroll
-        for (int q = 0; q < NG; ++q) {
-            uint32_t gi;
-            f.ok[q] = locate(f, t0, (uint32_t)q * 64 + lane, f.t[q], gi, f.j[q], f.rb[q], f.re[q]);
-            if (f.ok[q]) {
-                const uint32_t* tile = tiles + (uint64_t)f.t[q] * pl.tile_words;
-                __builtin_memcpy(&f.l[q], tile + gi * kGroupWords, 16);
-                f.nib[q] = tile[gi * kGroupWords + 4];
+            for (int q = 0; q < NG; ++q) {
+                const uint32_t c = (uint32_t)q * 64 + lane;
+                const uint32_t r1 = max(wave_incl_max_dpp((uint32_t)mk[c]), carry);
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)r1, 63);
+                f.ok[q] = c < f.total ? 1u : 0u;
+                if (f.ok[q]) {
+                    const uint4 ri = rinfo[wave][r1 - 1];
+                    f.rb[q] = ri.x;
+                    f.re[q] = ri.y;
+                    f.t[q] = std::min(t0 + r1 - 1, t_hi - 1);
+                    f.j[q] = c - ri.z;
+                    const uint32_t gi = ((ri.x & 0xFFFFu) >> 3) + f.j[q];
+                    const uint32_t* tile = tiles + (uint64_t)f.t[q] * pl.tile_words;
+                    __builtin_memcpy(&f.l[q], tile + gi * kGroupWords, 16);
+                    f.nib[q] = tile[gi * kGroupWords + 4];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NG; ++q) {
+                uint32_t gi;
+                f.ok[q] = locate(f, t0, (uint32_t)q * 64 + lane, f.t[q], gi, f.j[q], f.rb[q], f.re[q]);
+                if (f.ok[q]) {
+                    const uint32_t* tile = tiles + (uint64_t)f.t[q] * pl.tile_words;
+                    __builtin_memcpy(&f.l[q], tile + gi * kGroupWords, 16);
+                    f.nib[q] = tile[gi * kGroupWords + 4];
+                }
             }
         }
     };
