@@ -129,9 +129,9 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # 256 CUs x 4 SIMD32 x 2.4 GHz (int32
 # rocprofv3 names of the build's kernels, and the summary of the same command, per (key bytes, k)
 ROCPROF = {
     (16, 10): ({"tile_sort": "k_tile_pack<16, true, 10, true, false, 1, 0, 20, 0, false>",
-                "seg_or": "k_seg_or<6, 1024, 5, 8>"}, "profiles/r06/bench_default_kernel_stats.csv"),
+                "seg_or": "k_seg_or<7, 1024, 5, 8>"}, "profiles/r06/bench_default_kernel_stats.csv"),
     (16, 19): ({"tile_sort": "k_tile_pack<16, true, 19, true, false, 1, 0, 20, 0, false>",
-                "seg_or": "k_seg_or<6, 1024, 4, 8>"}, "profiles/r06/bench_k19_kernel_stats.csv"),
+                "seg_or": "k_seg_or<7, 1024, 4, 8>"}, "profiles/r06/bench_k19_kernel_stats.csv"),
 }
 
 
@@ -141,7 +141,7 @@ SQ_FILES = {10: "sq_tile_pack.json", 19: "sq_tile_pack_k19.json"}
 def pmc_sq(name, keys):
     """VALU issue busy, wait fractions and VALU lane-instructions per key of k_tile_pack from one
     rocprofv3 SQ pass (tools/pmc_sq.py) over a build of `keys` keys; the newest round's."""
-    for rnd in ("r05", "r04", "r03", "r02"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             with open(path) as f:
@@ -157,7 +157,7 @@ def pmc_sq(name, keys):
 def pmc_traffic(name, kernel=None):
     """HBM bytes measured by tools/pmc_traffic.py from rocprofv3 PMC passes (the newest round's
     measurement): (one launch of `kernel` -- read + write --, one whole build, source file)."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, name)
         try:
             with open(path) as f:

@@ -300,27 +300,17 @@ __global__ __launch_bounds__(BS) void k_seg_or(const uint32_t* tiles, const uint
         auto issue = [&](uint32_t t0, FB& b) {
             if constexpr (MK) {
                 // Round 6 (V = 7): the binary search costs 8 ds_bpermute per group -- more LDS
-                // instructions than the group's ORs.  Instead each run writes its bounds to rinfo and
-                // marks its first group slot (run + 1) in a byte table; a slot's run is then the max
-                // of the marks up to it (a DPP scan, carried across the NG slot rows) and its bounds
-                // one ds_read_b64: ~2 LDS instructions per group (tools/rdg6, profiles/r06/rdg6.log:
-                // -14 / -17 / -21 % at k = 10 / 19 / config 5).  Slots past 64 * NG keep the search
-                // (consume).  One wave's LDS operations run in order; the fences keep the compiler's.
-                uint8_t* mk = reinterpret_cast<uint8_t*>(marks[wave]);
-                for (uint32_t w = lane; w < NG * 16; w += 64) marks[wave][w] = 0;
+                // instructions than the group's ORs.  Instead the run marks (vbf_partition.hpp) and the
+                // run's bounds from rinfo: ~2 LDS instructions per group (tools/rdg6,
+                // profiles/r06/rdg6.log: -14 / -17 / -21 % at k = 10 / 19 / config 5).  Slots past
+                // 64 * NG keep the search (consume).
                 rinfo[wave][lane] = make_uint2(b.v, b.excl);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t st = b.v & 0xFFFFu, en = b.v >> 16;
-                if (en > st && b.excl < 64u * NG) mk[b.excl] = (uint8_t)(lane + 1);
-                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-                __builtin_amdgcn_wave_barrier();
+                run_marks_set<NG>(marks[wave], (b.v >> 16) > (b.v & 0xFFFFu), b.excl, lane);
                 uint32_t carry = 0;
 #pragma unroll
                 for (int q = 0; q < NG; ++q) {
                     const uint32_t c = (uint32_t)q * 64 + lane;
-                    const uint32_t r1 = max(wave_incl_max_dpp((uint32_t)mk[c]), carry);
-                    carry = (uint32_t)__builtin_amdgcn_readlane((int)r1, 63);
+                    const uint32_t r1 = run_marks_find(marks[wave], c, carry);
                     b.ab[q] = 0;
                     if (c < b.total) {  // r1 >= 1: some run starts at or before c
                         const uint2 ri = rinfo[wave][r1 - 1];

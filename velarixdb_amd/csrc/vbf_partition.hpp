@@ -92,6 +92,30 @@ __device__ __forceinline__ uint32_t wave_incl_max_dpp(uint32_t x) {
     return x;
 }
 
+// Run marks (round 6): the flattened segment readers deal a wave's runs' groups to lanes back to back
+// (slot c = 64 q + lane of row q < NG); the run owning a slot is found without ds_bpermute.  Each run
+// with groups marks its first slot (lane + 1) in the wave's byte table `marks` (NG * 16 words; runs
+// starting past the table mark nothing -- their slots take the caller's binary search), after the
+// caller wrote the runs' bounds to its own per-wave table; a slot's run is then the max of the marks
+// up to it, a DPP scan carried across the rows in order.  One wave's LDS operations run in order;
+// the fences keep the compiler's.
+template <int NG>
+__device__ __forceinline__ void run_marks_set(uint32_t* marks, bool has_groups, uint32_t excl, uint32_t lane) {
+    for (uint32_t w = lane; w < NG * 16; w += 64) marks[w] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (has_groups && excl < 64u * NG) reinterpret_cast<uint8_t*>(marks)[excl] = (uint8_t)(lane + 1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+// 1 + the lane of the run owning slot c (rows in order, carry starting at 0); >= 1 for every slot
+// below the batch's group total
+__device__ __forceinline__ uint32_t run_marks_find(const uint32_t* marks, uint32_t c, uint32_t& carry) {
+    const uint32_t r1 = max(wave_incl_max_dpp((uint32_t)reinterpret_cast<const uint8_t*>(marks)[c]), carry);
+    carry = (uint32_t)__builtin_amdgcn_readlane((int)r1, 63);
+    return r1;
+}
+
 // Exclusive scan of v[0..n) in LDS (n <= PER * blockDim.x, blockDim.x <= kPBlock).  EVEN: scan the
 // counts rounded up to even (the build's even-length runs) in the same pass.  One barrier: after
 // it every wave adds up the totals of the waves before it itself instead of waiting for one wave

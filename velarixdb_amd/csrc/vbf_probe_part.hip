@@ -223,6 +223,8 @@ template <int NG = 4>
 __global__ __launch_bounds__(kPBlock) void k_probe_seg2(const uint32_t* tiles, const uint16_t* endsT, uint32_t ntiles,
                                                         PartPlan pl, uint32_t G, const uint32_t* words, uint8_t* res) {
     __shared__ __attribute__((aligned(16))) uint32_t bitmap[kSegWords];
+    __shared__ __attribute__((aligned(16))) uint32_t marks[kPBlock / 64][NG * 16];
+    __shared__ __attribute__((aligned(16))) uint2 rinfo[kPBlock / 64][64];
     const uint32_t nwg = gridDim.x, qq = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
     const uint32_t wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + blockIdx.x / 8;
     const uint32_t seg = wg / G, part = wg % G;
@@ -269,15 +271,10 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg2(const uint32_t* tiles, c
     };
     auto prep = [&](uint32_t v, FB& b) {  // padded runs: whole groups
         const uint32_t ch = ((v >> 16) - (v & 0xFFFFu)) >> 3;
-        uint32_t incl = ch;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o);
-            if (lane >= (uint32_t)o) incl += y;
-        }
+        const uint32_t incl = wave_incl_scan_dpp(ch);
         b.v = v;
         b.excl = incl - ch;
-        b.total = (uint32_t)__shfl((int)incl, 63);
+        b.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     };
     auto locate = [&](const FB& b, uint32_t t0, uint32_t c, uint32_t& t, uint32_t& gi) -> uint32_t {
         uint32_t r = 0;
@@ -289,11 +286,19 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg2(const uint32_t* tiles, c
         gi = ((rv & 0xFFFFu) >> 3) + (c - rex);
         return c < b.total ? 1u : 0u;
     };
-    auto issue = [&](uint32_t t0, FB& b) {
+    auto issue = [&](uint32_t t0, FB& b) {  // round 6: the run marks (vbf_partition.hpp)
+        rinfo[wave][lane] = make_uint2(b.v, b.excl);
+        run_marks_set<NG>(marks[wave], (b.v >> 16) > (b.v & 0xFFFFu), b.excl, lane);
+        uint32_t carry = 0;
 #pragma unroll
         for (int q = 0; q < NG; ++q) {
-            b.ok[q] = locate(b, t0, (uint32_t)q * 64 + lane, b.t[q], b.gi[q]);
+            const uint32_t c = (uint32_t)q * 64 + lane;
+            const uint32_t r1 = run_marks_find(marks[wave], c, carry);
+            b.ok[q] = c < b.total ? 1u : 0u;
             if (b.ok[q]) {
+                const uint2 ri = rinfo[wave][r1 - 1];
+                b.t[q] = std::min(t0 + r1 - 1, t_hi - 1);
+                b.gi[q] = ((ri.x & 0xFFFFu) >> 3) + (c - ri.y);
                 const uint32_t* tile = tiles + (uint64_t)b.t[q] * pl.tile_words;
                 __builtin_memcpy(&b.l[q], tile + b.gi[q] * 5, 16);
                 b.nib[q] = tile[b.gi[q] * 5 + 4];

@@ -152,22 +152,15 @@ __global__ __launch_bounds__(kPBlock) void k_probe_seg3(const uint32_t* tiles, c
     const uint32_t wstep = (kPBlock / 64) * 64;
     auto issue = [&](uint32_t t0, FB& f) {
         if constexpr (MK) {
-            // each run marks its first group slot (run + 1) and leaves its bounds in rinfo; a slot's
-            // run is the max of the marks up to it (slots past 64 * NG: the search, in consume)
-            uint8_t* mk = reinterpret_cast<uint8_t*>(marks[wave]);
-            for (uint32_t w = lane; w < NG * 16; w += 64) marks[wave][w] = 0;
+            // the run marks (vbf_partition.hpp) and the runs' bounds in rinfo (slots past 64 * NG:
+            // the search, in consume)
             rinfo[wave][lane] = make_uint4(f.b, f.e, f.excl, 0u);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            if ((f.e & 0xFFFFu) > (f.b & 0xFFFFu) && f.excl < 64u * NG) mk[f.excl] = (uint8_t)(lane + 1);
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
+            run_marks_set<NG>(marks[wave], (f.e & 0xFFFFu) > (f.b & 0xFFFFu), f.excl, lane);
             uint32_t carry = 0;
 #pragma unroll
             for (int q = 0; q < NG; ++q) {
                 const uint32_t c = (uint32_t)q * 64 + lane;
-                const uint32_t r1 = max(wave_incl_max_dpp((uint32_t)mk[c]), carry);
-                carry = (uint32_t)__builtin_amdgcn_readlane((int)r1, 63);
+                const uint32_t r1 = run_marks_find(marks[wave], c, carry);
                 f.ok[q] = c < f.total ? 1u : 0u;
                 if (f.ok[q]) {
                     const uint4 ri = rinfo[wave][r1 - 1];
