@@ -230,9 +230,6 @@ __global__ __launch_bounds__(kPBlock) void k_group_seg2(const uint32_t* tiles, c
                                                         PartPlan pl, uint32_t G, const uint32_t* bytes, uint64_t nbytes,
                                                         uint8_t* res) {
     __shared__ __attribute__((aligned(16))) uint32_t seg_bytes[kByteSeg / 4];
-    // round 6: a group's run from the run marks (vbf_partition.hpp), not a ds_bpermute binary search
-    __shared__ __attribute__((aligned(16))) uint32_t marks[kPBlock / 64][NG * 16];
-    __shared__ __attribute__((aligned(16))) uint2 rinfo[kPBlock / 64][64];
     const uint8_t* sb = reinterpret_cast<const uint8_t*>(seg_bytes);
     const uint32_t nwg = gridDim.x, qq = nwg / 8, r8 = nwg % 8, xcd = blockIdx.x % 8;
     const uint32_t wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + blockIdx.x / 8;
@@ -296,14 +293,24 @@ __global__ __launch_bounds__(kPBlock) void k_group_seg2(const uint32_t* tiles, c
     auto prep = [&](uint32_t v, FB& b) {
         const uint32_t st = v & 0xFFFFu, en = v >> 16;
         const uint32_t ch = en > st ? ((en + 7) >> 3) - (st >> 3) : 0u;
-        const uint32_t incl = wave_incl_scan_dpp(ch);
+        uint32_t incl = ch;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= (uint32_t)o) incl += y;
+        }
         b.v = v;
         b.excl = incl - ch;
-        b.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        b.total = (uint32_t)__shfl((int)incl, 63);
     };
-    // group c of run r (bounds rv, first slot rex) -> tile, group index and live entries a | b << 4
-    auto place = [&](const FB& b, uint32_t t0, uint32_t c, uint32_t r, uint32_t rv, uint32_t rex, uint32_t& t,
-                     uint32_t& gi) -> uint32_t {
+    // (the run marks of k_seg_or, vbf_partition.hpp, measured 1.3 % slower in this pass, whose
+    // result-byte stores bound it: profiles/r06/ab_marks_multi.log)
+    auto locate = [&](const FB& b, uint32_t t0, uint32_t c, uint32_t& t, uint32_t& gi) -> uint32_t {
+        uint32_t r = 0;
+#pragma unroll
+        for (int sft = 32; sft; sft >>= 1)
+            if ((uint32_t)__shfl((int)b.excl, (int)r + sft) <= c) r += sft;
+        const uint32_t rv = (uint32_t)__shfl((int)b.v, (int)r), rex = (uint32_t)__shfl((int)b.excl, (int)r);
         const uint32_t rst = rv & 0xFFFFu, ren = rv >> 16;
         t = std::min(t0 + r, t_hi - 1);
         gi = (rst >> 3) + (c - rex);
@@ -311,27 +318,10 @@ __global__ __launch_bounds__(kPBlock) void k_group_seg2(const uint32_t* tiles, c
         const uint32_t a = gi * 8 < rst ? rst - gi * 8 : 0u, e = std::min<uint32_t>(8, ren - gi * 8);
         return a | (e << 4);
     };
-    auto locate = [&](const FB& b, uint32_t t0, uint32_t c, uint32_t& t, uint32_t& gi) -> uint32_t {
-        uint32_t r = 0;
-#pragma unroll
-        for (int sft = 32; sft; sft >>= 1)
-            if ((uint32_t)__shfl((int)b.excl, (int)r + sft) <= c) r += sft;
-        const uint32_t rv = (uint32_t)__shfl((int)b.v, (int)r), rex = (uint32_t)__shfl((int)b.excl, (int)r);
-        return place(b, t0, c, r, rv, rex, t, gi);
-    };
     auto issue = [&](uint32_t t0, FB& b) {
-        rinfo[wave][lane] = make_uint2(b.v, b.excl);
-        run_marks_set<NG>(marks[wave], (b.v >> 16) > (b.v & 0xFFFFu), b.excl, lane);
-        uint32_t carry = 0;
 #pragma unroll
         for (int q = 0; q < NG; ++q) {
-            const uint32_t c = (uint32_t)q * 64 + lane;
-            const uint32_t r1 = run_marks_find(marks[wave], c, carry);
-            b.ab[q] = 0;
-            if (c < b.total) {
-                const uint2 ri = rinfo[wave][r1 - 1];
-                b.ab[q] = place(b, t0, c, r1 - 1, ri.x, ri.y, b.t[q], b.gi[q]);
-            }
+            b.ab[q] = locate(b, t0, (uint32_t)q * 64 + lane, b.t[q], b.gi[q]);
             if (b.ab[q]) {
                 const uint32_t* tile = tiles + (uint64_t)b.t[q] * pl.tile_words;
                 __builtin_memcpy(&b.l[q], tile + b.gi[q] * 5, 16);
