@@ -8,6 +8,7 @@ stores.  Usage: pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON
 """
 import collections
 import csv
+import re
 import json
 import sys
 
@@ -30,8 +31,9 @@ def main(fetch_csv, write_csv, out):
     for name in sorted(set(fetch) | set(write)):
         if not any(b in name for b in BUILD_KERNELS):
             continue
-        # the probes' position-table pack (round 4; POS, then SAT in the name)
-        if any(t in name for t in (", 20, true>", ", 17, true>", ", 20, true, false>", ", 17, true, false>")):
+        # the probes' packs: k_tile_pack with POS = 1 (round 4) or 2 (round 6) -- POS is the template
+        # argument after the segment bits (17 / 20), then SAT; round 4-5 names had POS as a bool
+        if re.search(r", (17|20), (true|1|2)(, (true|false))?>", name):
             continue
         rd = fetch.get(name, 0.0) * 1024 * 2
         wr = write.get(name, 0.0) * 1024
