@@ -112,7 +112,11 @@ int vbf_probe_dev(const uint8_t* keys, const uint64_t* offsets, uint64_t stride,
 int vbf_build_dev_ex(const uint8_t* keys, const uint64_t* offsets, uint64_t stride, uint64_t n,
                      int len_prefix, uint32_t m, uint32_t k, uint32_t* words, int strategy,
                      void* stream);
-/* Device bytes the partitioned build of n keys needs as workspace (0 if unsupported). */
+/* Device bytes the partitioned build of n keys needs as workspace (0 if unsupported): the tile
+ * image (~2.6 bytes per bit index) and the run ends of one build chunk of up to 2^32 bit indices
+ * -- about 11 GB for a chunk of 2^32 indices (config 5's 1B keys at k = 4), kept per stream until
+ * vbf_release_workspaces.  When that allocation fails the build retries with half the chunk, down
+ * to 2^28 indices (VBF_WS_MAX_BYTES caps the workspace the same way). */
 uint64_t vbf_build_workspace_bytes(uint64_t n, uint32_t m, uint32_t k);
 /* Free every cached workspace (synchronizes the streams that own them). */
 int vbf_release_workspaces(void);
