@@ -79,6 +79,7 @@ for s in $STEPS; do
     abparity) run pytest_ab_parity 900 env VBF_LIB=velarixdb_amd/libvbf_ab.so python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     ablatesst) run ablate_sst 300 python tools/ablate_sst.py ;;
     probephases) run probe_phases 300 python tools/probe_phases.py 10 && run probe_phases19 300 python tools/probe_phases.py 19 ;;
+    probephases94) run probe_phases9 300 python tools/probe_phases.py 9 && run probe_phases4 300 python tools/probe_phases.py 4 ;;
     probephasesk) run probe_phases14 300 python tools/probe_phases.py 14 && run probe_phases7 300 python tools/probe_phases.py 7 && run probe_phases21 300 python tools/probe_phases.py 21 ;;
     benchatomic) run bench_atomic 300 python bench.py --no-cpu-baseline --strategy 1 --steps 3 ;;
     bench3) run bench_cfg3 600 python bench.py --config 3 --steps 5 --warmup 1 ;;

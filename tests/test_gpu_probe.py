@@ -188,6 +188,8 @@ SAT = 4_294_967_295
     (16, 300_000_007, 14, 1_000_000, None), (32, 50_000_017, 7, 600_000, None), (8, 40_000_003, 32, 200_000, None),
     (24, 100_000_007, 23, 400_000, None), (16, 1 << 31, 12, 500_000, None), (16, 200_000_003, 5, 900_000, None),
     (32, 150_000_001, 21, 300_000, "22"),
+    # k = 4 and 9 below 2^32 - 1 (no compiled pack there): the classes 5 and 12
+    (16, 300_000_001, 9, 3_000_000, None), (32, 200_000_011, 4, 5_000_000, None), (None, 400_000_009, 9, 800_000, None),
     # runtime key lengths: the offsets layout (keys dealt to lanes in length order; the answers go
     # back through the slot -> key map) and an odd fixed stride (13 B: the runtime-stride layout)
     (None, SAT, 4, 800_000, None), (None, 1_000_000_000, 10, 1_000_000, None), (None, 1_900_000_000, 19, 500_000, None),
@@ -202,7 +204,8 @@ def test_round6_probe_on_build_image(vbf, ora, L, m, k, n, chunk_log2):
     bf.rs:230-233; k = 4) with single keys, tile edges (6 532 keys per tile) and several chunks;
     k = 10 / 19 with one segment (m = 5 000: every tile's runs split over many workgroups), the
     largest m of the path (2^31) and several chunks; every runtime-k class (the K1 class kernels with
-    the class's slots per key, k at run time); variable-length keys (the pack's length order, the
+    the class's slots per key, k at run time), k = 4 and 9 below 2^32 - 1 included (classes 5 and
+    12); variable-length keys (the pack's length order, the
     answers mapped back to key order) and an odd fixed stride.  Anchor: contains(), bf.rs:95-105."""
     import torch
     from velarixdb_amd._lib import call

@@ -551,9 +551,14 @@ static PartPlan make_plan(uint32_t m, uint32_t k, bool fixed = true, bool lp = t
     if (k14env == 1 && satenv != 0 && k == 4 && fixed && lp && m == 0xFFFFFFFFu && !group && pl.c16) pl.k1v = 1;
     // the round-6 probe pack (K1 with POS = 2, vbf_probe_pu.hip): one u32 counter per segment (the
     // run's place and padded place in its two halves)
-    if (pu) {  // k = 4: the 1 024-thread shape; k = 10 / 19 keep the build's 512-thread one
+    if (pu) {  // k = 4 at m = 2^32 - 1: the 1 024-thread shape; k = 10 / 19 keep the build's 512-thread one
         pl.c16 = 0;
-        if (k == 4) pl.k1v = 0;
+        if (k == 4 && m == 0xFFFFFFFFu) {
+            pl.k1v = 0;
+        } else if ((k == 4 || k == 9) && kcls != 0) {  // below it the pack has no compiled k = 4 / 9: a class
+            pl.kc = tile_pack_class(k);
+            pl.k1v = 1;
+        }
     }
     const K1Shape sh = k1_shape((int)(pl.kc ? pl.kc : k), fixed, (int)pl.k1v);
     const uint32_t rmax = (uint32_t)(ck || pl.kc ? sh.rounds : rounds_max((int)k));

@@ -323,7 +323,8 @@ __global__ __launch_bounds__(kPBlock) void k_probe_out3(const uint8_t* res, cons
 //   k = 4 at m = 2^32 - 1 (config 5: SAT remainders, the 1 024-thread shape, seven stash rounds);
 //   k = 10 and 19 (p = 1e-4, velarixdb's default) at m <= 2^31: the build's 512-thread
 //   one-lane-per-key shape with its full tile -- where the round-4 pipeline (vbf_probe_part.hip)
-//   reserves 7 entries of LDS per segment for run padding.
+//   reserves 7 entries of LDS per segment for run padding;
+//   any other k <= 32 at m <= 2^31 (k = 4 and 9 too): the runtime-k class packs (_rk_a / _rk_b).
 // Other batches take the round-3 / round-4 pipelines; VBF_PROBE_PU = 0 keeps them for these too (A/B).
 static bool pu_shape(const PartPlan& pl, bool lp) {
     if (!lp || pl.c16 || !pl.ends_t) return false;
@@ -336,7 +337,8 @@ bool probe_pu_enabled(uint32_t m, uint32_t k, bool lp, bool fixed) {
     const char* e = getenv("VBF_PROBE_PU");  // read per call (A/B)
     static const int sat = [] { const char* v = getenv("VBF_SAT"); return v ? atoi(v) : 1; }();
     if ((e && atoi(e) == 0) || !lp || m == 0) return false;
-    const bool cls = k != 4 && k != 9 && k != 10 && k != 19 && tile_pack_class(k) != 0;
+    // every k but 10 / 19 below 2^32 - 1 runs a runtime-k class pack (k = 4 and 9 included)
+    const bool cls = k != 10 && k != 19 && tile_pack_class(k) != 0;
     (void)fixed;
     if (!((k == 4 && m == 0xFFFFFFFFu && sat) || ((k == 10 || k == 19 || cls) && m <= (1u << 31)))) return false;
     const PartPlan pl = make_probe_pu_plan(m, k, fixed, lp);
