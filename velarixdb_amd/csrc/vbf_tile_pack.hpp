@@ -82,6 +82,7 @@ __device__ __forceinline__ void length_order(const DevKeys& dk, uint64_t key0, u
 }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
 // The tile image is read back only by k_seg_or after this launch (2.5 GB at config 2: far beyond
 // the L2 and the Infinity Cache), so its copy-out is a streaming store (VBF_IMAGE_NT, default on):
@@ -415,13 +416,18 @@ __global__ __launch_bounds__(V == 1 ? 512 : kPBlock, V == 1 ? 4 : 8) void k_tile
             for (int q = 0; q < 8; ++q)
                 if (val[q] != kSentinel) pos[q] += gd_get(val[q] >> SB);
         }
+        // the image addresses as 32-bit LDS byte addresses from LDS address 0 (a generic pointer's
+        // index took a 64-bit v_mad_u64_u32 per entry); p < 2^16, so a 24-bit multiply
+        const uint32_t img0 = (cnt_words + 16 + kLenBuckets + pl.gd_words) * 4u;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (val[q] != kSentinel) {
                 const uint32_t p = POS == 2 ? pos[q] & 0xFFFFu : pos[q];
-                const uint32_t g = (p >> 3) * kGroupWords, e7 = p & 7;
-                lo[g * 2 + e7] = (uint16_t)val[q];
-                atomicOr(&smem[g + 4], ((val[q] >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4));
+                const uint32_t gb = img0 + __umul24(p >> 3, kGroupWords * 4), e7 = p & 7;
+                *reinterpret_cast<lds_u16*>((uintptr_t)(gb + e7 * 2)) = (uint16_t)val[q];
+                (void)__hip_atomic_fetch_or(reinterpret_cast<lds_u32*>((uintptr_t)(gb + 16)),
+                                            ((val[q] >> 16) & ((1u << (SB - 16)) - 1u)) << (e7 * 4), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
         if constexpr (POS != 0) {  // coalesced: for a pair of stash slots the lanes write consecutive u32
