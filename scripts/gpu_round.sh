@@ -64,6 +64,10 @@ for s in $STEPS; do
     abprev3) run ab_prev3 600 env AB_LIB=velarixdb_amd/libvbf_prev.so tools/ab_lib.sh 2 --config 3 --steps 5 --warmup 1 ;;
     abprev5) for i in 1 2; do for lib in "" velarixdb_amd/libvbf_prev.so; do run bench_cfg5_prev$i${lib:+_prev} 600 env VBF_LIB=$lib python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline; grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_cfg5_prev$i${lib:+_prev}.log"; done; done ;;
     abprevmulti) for i in 1 2; do for lib in "" velarixdb_amd/libvbf_prev.so; do run bench_multi_prev$i${lib:+_prev} 300 env VBF_LIB=$lib python bench.py --multi --steps 10 --warmup 2; grep -o '"ms_per_step": [0-9.]*\|"phases".*' "$OUT/bench_multi_prev$i${lib:+_prev}.log" | cut -c1-400; done; done ;;
+    abpasses) run ab_passes_parity 900 env AB_PARITY=1 AB_ENVS="VBF_K3_PASSES=4" bash tools/env_ab.sh
+              run ab_passes10 600 env AB_ENVS="VBF_K3_PASSES=1 VBF_K3_PASSES=2 VBF_K3_PASSES=4 VBF_K3_PASSES=1 VBF_K3_PASSES=2 VBF_K3_PASSES=4" bash tools/env_ab.sh
+              run ab_passes19 600 env AB_ENVS="VBF_K3_PASSES=1 VBF_K3_PASSES=2 VBF_K3_PASSES=4 VBF_K3_PASSES=1 VBF_K3_PASSES=2 VBF_K3_PASSES=4" AB_ARGS="--bits-per-key 19" bash tools/env_ab.sh ;;
+    abpasses5) for v in 1 4 2 8 1 4; do run bench_cfg5_passes$v 600 env VBF_K3_PASSES=$v python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline; echo "VBF_K3_PASSES=$v"; grep -o '"ms_per_step": [0-9.]*\|"phases": {[^}]*}[^}]*}' "$OUT/bench_cfg5_passes$v.log" | head -2; done ;;
     probe5) run bench_cfg5_probe 600 python bench.py --config 5 --steps 3 --warmup 1 --no-cpu-baseline ;;
     probemultitests) run pytest_probe_multi 900 python -u -m pytest tests/test_gpu_probe.py tests/test_gpu_multi.py tests/test_gpu_parity.py tests/test_gpu_scale.py -x -q -m gpu --timeout 300 --timeout-method thread ;;
     probetests) run pytest_probe_sat 900 python -u -m pytest tests/test_gpu_probe.py -x -q -m gpu --timeout 300 --timeout-method thread ;;

@@ -834,8 +834,22 @@ hipError_t launch_build_partitioned(const KeyBatch& kb, uint32_t m, uint32_t k, 
                 : k3v == 1 ? k_seg_or<0>
                            : k_seg_or<3, kPBlock, 5>;
         const int bs = (k3v == 5 || k3v == 6) ? 768 : kPBlock;
-        hipLaunchKernelGGL(k3, dim3(pl.nfull + (pl.nseg - pl.nfull) * pl.P), dim3(bs), 0, s, tiles, endsT, ntiles,
-                           pl, merge, words);
+        // VBF_K3_PASSES = q (experiments, speed only): the segment pass in q launches over consecutive
+        // tile windows -- each launch boundary re-aligns the workgroups that share tile lines in an
+        // XCD's L2 (they drift apart within one launch); every window after the first reads the
+        // segment's words back (the previous window's result) and writes them again
+        static const uint32_t k3passes = [] {
+            const char* e = getenv("VBF_K3_PASSES");
+            return (uint32_t)std::max(1, e ? atoi(e) : 1);
+        }();
+        const uint32_t passes = std::max<uint32_t>(1, std::min<uint32_t>(k3passes, ntiles / std::max<uint32_t>(pl.P, 16)));
+        for (uint32_t ps = 0; ps < passes; ++ps) {
+            const uint32_t a = (uint32_t)((uint64_t)ntiles * ps / passes), b = (uint32_t)((uint64_t)ntiles * (ps + 1) / passes);
+            PartPlan pp = pl;
+            if (ps > 0) pp.fresh = 0;
+            hipLaunchKernelGGL(k3, dim3(pl.nfull + (pl.nseg - pl.nfull) * pl.P), dim3(bs), 0, s,
+                               tiles + (uint64_t)a * pl.tile_words, endsT + a, b - a, pp, merge, words);
+        }
         phase_end(kPhaseSegOr, s);
         err = hipGetLastError();
         if (err != hipSuccess) return err;
